@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""North-star benchmark: Gsamples/s of the causal moving average on MI355X.
+
+BASELINE.json metric: "Gsamples/s moving-average (N=2^30 fp32, k=1024);
+achieved HBM GB/s vs peak".  A step is one pass of the hot path over one
+batch: (N>1) the (k-1)-sample halo exchange with the neighbour rank over
+RCCL, then one libmavg launch over this rank's 2^30-sample shard, inputs
+already resident in HBM (generated on the device by the counter-based
+synthetic generator).  Weak scaling: 2^30 samples per GPU.
+
+    python bench.py                      # N=1, default K/W
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line (contract in the task statement), with
+`roofline` (dominant kernel, algorithmic bytes / HIP-event kernel time vs
+8 TB/s) and `cpu_baseline` (oracle restatement on a bounded sample, 1 core).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Gsamples/s moving-average (N=2^30 fp32, k=1024); achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOADS = {
+    # name: (samples per GPU, k, channels, dtype, default algo)
+    "headline": (1 << 30, 1024, 1, "f32", "blelloch"),      # configs[4] per GPU / metric config
+    "blelloch_2p26": (1 << 26, 64, 1, "f32", "blelloch"),   # configs[1]
+    "direct_2p28": (1 << 28, 7, 1, "f32", "direct"),        # configs[2]
+    "carry_2p30": (1 << 30, 4096, 1, "f32", "blelloch"),    # configs[3]
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="headline", choices=sorted(WORKLOADS))
+    ap.add_argument("--algo", default=None, help="override the workload's algorithm")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-samples", type=int, default=1 << 28, help="bounded CPU-baseline sample (samples)")
+    ap.add_argument("--cpu-reps", type=int, default=5)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--all-workloads", action="store_true",
+                    help="print one extra JSON line per secondary workload (rank 0, N=1 only)")
+    return ap.parse_args()
+
+
+def init_dist(args):
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def barrier(world):
+    import torch
+    import torch.distributed as dist
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize()
+
+
+def max_over_ranks(v: float, world: int) -> float:
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def load_traffic(path, workload, algo):
+    """HBM bytes per launch from the committed PMC summary (profiles/), or None."""
+    try:
+        with open(path) as f:
+            data = json.load(f)
+        ent = data.get(f"{workload}:{algo}")
+        return None if ent is None else float(ent["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def cpu_baseline(args, n_total, k, C, seed):
+    """Oracle restatement (profilable_moving_averager.cpp:14-37, fp64 running
+    sum) on a bounded sample of the same synthetic stream, one host core."""
+    import oracle
+    oracle.build()
+    n = min(args.cpu_samples, n_total)
+    x = oracle.synth_f32(n, seed=seed)
+    oracle.mavg_f32(x[: min(n, 1 << 20)], k, C)  # warm the code path
+    times = []
+    for _ in range(args.cpu_reps):
+        t = time.perf_counter()
+        oracle.mavg_f32(x, k, C)
+        times.append(time.perf_counter() - t)
+    med = statistics.median(times)
+    return {
+        "value": round(n / med / 1e9, 4),
+        "unit": "Gsamples/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{n} fp32 samples (first {n} of the benchmark's synthetic stream), k={k}, C={C}, "
+                  f"median of {args.cpu_reps} reps, {med * 1e3:.1f} ms/rep, single thread",
+    }
+
+
+def run_workload(args, name, rank, world, with_cpu):
+    import torch
+    import digital_signal_processsing_amd as dsp
+    from digital_signal_processsing_amd.shard import exchange_halo
+
+    n, k, C, dt, algo = WORKLOADS[name]
+    if args.algo and name == args.workload:
+        algo = args.algo
+    seed = 0x5EED
+    dtype = torch.float32 if dt == "f32" else torch.int16
+    # weak scaling: this rank holds global samples [rank*n, (rank+1)*n)
+    x = dsp.fill_synthetic(n, dtype, seed=seed, offset=rank * n, device="cuda")
+    y = torch.empty_like(x)
+    hist_buf = torch.empty(max((k - 1) * C, 1), dtype=dtype, device="cuda")
+    resolved = dsp.resolve_algo(n, k, C, dsp.F32 if dt == "f32" else dsp.I16, algo)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+
+    def step(i=None):
+        hist = exchange_halo(x, k, C, recv_buf=hist_buf[: (k - 1) * C]) if world > 1 else None
+        if i is not None:
+            ev[i][0].record()
+        dsp.moving_average_into(x, y, k, C, algo, history=hist)
+        if i is not None:
+            ev[i][1].record()
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    barrier(world)
+    dt_s = time.perf_counter() - t0
+    dt_s = max_over_ranks(dt_s, world)
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_avg_ms = statistics.mean(kern_ms)
+    kern_avg_ms = max_over_ranks(kern_avg_ms, world)
+
+    elem = 4 if dt == "f32" else 2
+    alg_bytes = 2 * elem * n  # read x once, write y once
+    achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
+    total_samples = n * world * args.steps
+    value = total_samples / dt_s / 1e9
+    traffic = load_traffic(args.traffic_json, name, resolved)
+    line = {
+        "metric": METRIC if name == "headline" else f"Gsamples/s moving-average ({name})",
+        "value": round(value, 3),
+        "unit": "Gsamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt_s * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dt,
+        "data": "synthetic (device counter-based splitmix64, int16-valued samples)",
+        "config": {
+            "workload": f"{name}: {n} {dt} samples per GPU, k={k}, C={C}, algo={resolved}",
+            "n_samples_per_gpu": n,
+            "n_samples_total": n * world,
+            "k": k,
+            "channels": C,
+            "algo": resolved,
+            "parallelism": f"shard{world} (contiguous shards, (k-1)-sample RCCL halo)" if world > 1 else "single GPU",
+        },
+        "hbm_gbs_algorithmic": round(alg_bytes * world * args.steps / dt_s / 1e9, 1),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": f"scan_kernel/{resolved}" if "direct" not in resolved else f"direct_kernel/{resolved}",
+            "kernel_avg_ms": round(kern_avg_ms, 4),
+            "kernel_min_ms": round(min(kern_ms), 4),
+            "algorithmic_bytes_per_launch": alg_bytes,
+        },
+    }
+    if with_cpu and rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args, n, k, C, seed)
+    del x, y
+    torch.cuda.empty_cache()
+    return line
+
+
+def main():
+    args = parse()
+    rank, world, _ = init_dist(args)
+    line = run_workload(args, args.workload, rank, world, with_cpu=True)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if args.all_workloads and world == 1:
+        for name in sorted(WORKLOADS):
+            if name != args.workload:
+                extra = run_workload(args, name, rank, world, with_cpu=False)
+                print(json.dumps(extra), file=sys.stderr, flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

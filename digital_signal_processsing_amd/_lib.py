@@ -1,0 +1,119 @@
+"""ctypes binding of libmavg (include/mavg.h).
+
+The library is built in-tree (``digital_signal_processsing_amd/lib/libmavg.so``)
+by ``build.py``; there is no fallback path: if the library is missing or
+fails to load, every entry point raises ``MavgLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "lib", "libmavg.so")
+
+# mavg_dtype
+I16 = 0
+F32 = 1
+
+# mavg_algo (include/mavg.h)
+ALGO_AUTO = 0
+ALGO_BLELLOCH = 1
+ALGO_BLELLOCH_SCALAR = 2
+ALGO_HILLIS = 3
+ALGO_HILLIS_SCALAR = 4
+ALGO_DIRECT = 5
+ALGO_DIRECT_VEC2 = 6
+ALGO_DIRECT_SCALAR = 7
+ALGO_NAIVE = 8
+
+ALGOS = {
+    "auto": ALGO_AUTO,
+    "blelloch": ALGO_BLELLOCH,
+    "blelloch_scalar": ALGO_BLELLOCH_SCALAR,
+    "hillis": ALGO_HILLIS,
+    "hillis_scalar": ALGO_HILLIS_SCALAR,
+    "direct": ALGO_DIRECT,
+    "direct_vec2": ALGO_DIRECT_VEC2,
+    "direct_scalar": ALGO_DIRECT_SCALAR,
+    "naive": ALGO_NAIVE,
+}
+
+# mavg_status
+OK = 0
+ERR_INVALID_ARG = 1
+ERR_UNSUPPORTED = 2
+ERR_MISALIGNED = 3
+ERR_WORKSPACE = 4
+ERR_HIP = 5
+
+# every symbol include/mavg.h declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = (
+    "mavg_workspace_bytes",
+    "mavg_run",
+    "mavg_resolve_algo",
+    "mavg_fill_synthetic",
+    "mavg_strerror",
+    "mavg_algo_name",
+    "mavg_abi_version",
+)
+
+
+class MavgLibraryError(RuntimeError):
+    """libmavg.so is missing or failed to load (no CPU fallback exists)."""
+
+
+class MavgError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: {strerror(status)} (status {status})")
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MavgLibraryError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the runtime image
+        raise MavgLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+    vp, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+    lib.mavg_workspace_bytes.argtypes = [sz, i, i, i, i, i, ctypes.POINTER(sz)]
+    lib.mavg_workspace_bytes.restype = i
+    lib.mavg_run.argtypes = [vp, vp, sz, i, i, i, i, i, vp, vp, sz, vp]
+    lib.mavg_run.restype = i
+    lib.mavg_resolve_algo.argtypes = [sz, i, i, i, i]
+    lib.mavg_resolve_algo.restype = i
+    lib.mavg_fill_synthetic.argtypes = [vp, sz, i, u64, u64, i, vp]
+    lib.mavg_fill_synthetic.restype = i
+    lib.mavg_strerror.argtypes = [i]
+    lib.mavg_strerror.restype = ctypes.c_char_p
+    lib.mavg_algo_name.argtypes = [i]
+    lib.mavg_algo_name.restype = ctypes.c_char_p
+    lib.mavg_abi_version.argtypes = []
+    lib.mavg_abi_version.restype = i
+    _lib = lib
+    return lib
+
+
+def strerror(status: int) -> str:
+    try:
+        return load().mavg_strerror(status).decode()
+    except MavgLibraryError:
+        return f"status {status}"
+
+
+def algo_name(algo: int) -> str:
+    return load().mavg_algo_name(algo).decode()
+
+
+def check(status: int, what: str) -> None:
+    if status != OK:
+        raise MavgError(status, what)

@@ -1,0 +1,608 @@
+// mavg_kernels.hpp -- hand-written HIP kernels for gfx950 (CDNA4, wave64).
+//
+// The hot path: causal k-frame moving average over interleaved C-channel
+// signals, y[f,c] = S[f,c] / k with S[f,c] = sum_{j<k} x[(f-j)C + c]
+// (reference semantics: basics/profilable_moving_averager.cpp:14-37).
+//
+// Kernels
+//   scan_kernel    single-pass STREAMING scan (replaces the reference's
+//                  multi-launch recursive Blelloch / Hillis-Steele pipelines,
+//                  blelloch_scan_averager.cu:40-186, hillis_steele_averager.cu:17-100).
+//                  Each 256-thread workgroup owns a contiguous segment of
+//                  frames and walks it chunk by chunk:
+//                    d[n] = x[n] - x[n-k]          (x[n-k] from an LDS ring)
+//                    W[n] = W[n-1] + d[n]          (scan of d, fp64 / int32)
+//                  The scan is hierarchical: serial in-lane over F frames,
+//                  64-lane DPP inclusive scan of lane totals (Blelloch flavour)
+//                  or element-wise log-step __shfl_up scan (Hillis-Steele
+//                  flavour), an LDS exchange of the 4*U wave-segment totals,
+//                  and a register carry from chunk to chunk.  The carry into
+//                  a segment is recomputed from a k-frame pre-roll instead of
+//                  being propagated between workgroups, so there is no
+//                  inter-workgroup communication at all (no look-back, no
+//                  grid sync): 8 B/sample of HBM traffic in fp32, 4 B/sample
+//                  in int16, plus k/segment of pre-roll re-read.
+//   direct_kernel  LDS-tiled direct window sum (replaces profilable_sm_*.cu):
+//                  a tile plus its (k-1)-frame halo is staged in LDS with
+//                  16/8/4-B loads; each thread sums k frames per output.
+//   naive_kernel   one thread per sample, window read from global memory
+//                  (replaces profilable_parallel_averager.cu:14-23).
+//   synth_kernel   counter-based synthetic input (splitmix64).
+//
+// Arithmetic: fp32 data accumulates in fp64 (a global fp32 prefix loses
+// 1e-4..1e-1 relative); int16 data accumulates exactly in
+// int32 (k <= 65535) or int64, and divides with a magic-number multiply that
+// is exact truncating division (NOT the reference's float reciprocal, which
+// is off on exact multiples: SURVEY.md 0.4).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mavg {
+
+constexpr int kWG = 256;          // threads per workgroup (4 wave64s)
+constexpr int kNW = kWG / 64;     // waves per workgroup
+
+// ----------------------------------------------------------------------------
+// small helpers
+// ----------------------------------------------------------------------------
+template <typename T> struct AccFor;
+template <> struct AccFor<float> { using type = double; };
+template <> struct AccFor<int16_t> { using type = int32_t; };
+
+template <typename A> __device__ __forceinline__ A to_acc(float x) { return (A)x; }
+template <typename A> __device__ __forceinline__ A to_acc(int16_t x) { return (A)x; }
+
+// 64-lane DPP move with zero fill for invalid / masked lanes.
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int32_t dpp(int32_t v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, BM, false);
+}
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ double dpp(double v) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, BM, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, BM, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int64_t dpp(int64_t v) {
+  int lo = (int)(uint32_t)v, hi = (int)(uint32_t)((uint64_t)v >> 32);
+  lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, BM, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, BM, false);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// Inclusive scan across the 64 lanes of a wave: Kogge-Stone inside each
+// 16-lane row (row_shr 1,2,4,8) then row_bcast:15 / row_bcast:31 to carry
+// row totals across rows -- 6 DPP steps, no LDS.
+template <typename A>
+__device__ __forceinline__ A wave_incl_scan(A v) {
+  v += dpp<0x111, 0xf, 0xf>(v);
+  v += dpp<0x112, 0xf, 0xf>(v);
+  v += dpp<0x114, 0xf, 0xf>(v);
+  v += dpp<0x118, 0xf, 0xf>(v);
+  v += dpp<0x142, 0xa, 0xf>(v);
+  v += dpp<0x143, 0xc, 0xf>(v);
+  return v;
+}
+
+__device__ __forceinline__ int32_t readlane(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ double readlane(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ int64_t readlane(int64_t v, int l) {
+  uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ double shfl_up(double v, int d) { return __shfl_up(v, d, 64); }
+__device__ __forceinline__ int32_t shfl_up(int32_t v, int d) { return __shfl_up(v, d, 64); }
+__device__ __forceinline__ int64_t shfl_up(int64_t v, int d) {
+  return (int64_t)__shfl_up((long long)v, d, 64);
+}
+
+// ----------------------------------------------------------------------------
+// output conversion: window sum -> sample
+// ----------------------------------------------------------------------------
+struct OutParams {
+  double inv_k;     // 1/k (fp32 output, int64 path estimate)
+  uint32_t magic;   // int16/int32 path: q = umulhi(|S|, magic) >> shift
+  int shift;
+  int k;            // divisor
+};
+
+__device__ __forceinline__ float to_out_f32(double s, const OutParams& o) {
+  return (float)(s * o.inv_k);
+}
+// exact C++ truncating division S / k for |S| < 2^31, k <= 65535
+__device__ __forceinline__ int16_t to_out_i16(int32_t s, const OutParams& o) {
+  uint32_t a = s < 0 ? (uint32_t)(-s) : (uint32_t)s;
+  uint32_t q = (o.k == 1) ? a : (__umulhi(a, o.magic) >> o.shift);
+  return (int16_t)(s < 0 ? -(int32_t)q : (int32_t)q);
+}
+// exact truncating division for |S| < 2^53 (large-k int16 path)
+__device__ __forceinline__ int16_t to_out_i16(int64_t s, const OutParams& o) {
+  int64_t a = s < 0 ? -s : s;
+  int64_t q = (int64_t)((double)a * o.inv_k);
+  int64_t r = a - q * (int64_t)o.k;
+  while (r >= o.k) { ++q; r -= o.k; }
+  while (r < 0) { --q; r += o.k; }
+  return (int16_t)(s < 0 ? -q : q);
+}
+template <typename T, typename A>
+__device__ __forceinline__ T to_out(A s, const OutParams& o);
+template <> __device__ __forceinline__ float to_out<float, double>(double s, const OutParams& o) { return to_out_f32(s, o); }
+template <> __device__ __forceinline__ int16_t to_out<int16_t, int32_t>(int32_t s, const OutParams& o) { return to_out_i16(s, o); }
+template <> __device__ __forceinline__ int16_t to_out<int16_t, int64_t>(int64_t s, const OutParams& o) { return to_out_i16(s, o); }
+
+// ----------------------------------------------------------------------------
+// a "unit" = the F frames x C channels one lane owns per load instruction
+// ----------------------------------------------------------------------------
+template <typename T, int VE>
+struct Unit {
+  T e[VE];
+};
+
+template <int BYTES> struct RawVec;
+template <> struct RawVec<16> { using type = uint4; };
+template <> struct RawVec<8> { using type = uint2; };
+template <> struct RawVec<4> { using type = uint32_t; };
+template <> struct RawVec<2> { using type = uint16_t; };
+
+template <typename T, int VE>
+struct UnitIO {
+  static constexpr int kBytes = VE * (int)sizeof(T);
+  static constexpr bool kVec = (kBytes == 16 || kBytes == 8 || kBytes == 4 || kBytes == 2);
+
+  // p is aligned to kBytes when kVec (checked on the host for the base pointer)
+  __device__ __forceinline__ static Unit<T, VE> load(const T* __restrict__ p) {
+    Unit<T, VE> u;
+    if constexpr (kVec) {
+      using R = typename RawVec<kBytes>::type;
+      R r = *reinterpret_cast<const R*>(p);
+      __builtin_memcpy(&u, &r, kBytes);
+    } else {
+#pragma unroll
+      for (int i = 0; i < VE; ++i) u.e[i] = p[i];
+    }
+    return u;
+  }
+  __device__ __forceinline__ static void store(T* __restrict__ p, const Unit<T, VE>& u) {
+    if constexpr (kVec) {
+      using R = typename RawVec<kBytes>::type;
+      R r;
+      __builtin_memcpy(&r, &u, kBytes);
+      *reinterpret_cast<R*>(p) = r;
+    } else {
+#pragma unroll
+      for (int i = 0; i < VE; ++i) p[i] = u.e[i];
+    }
+  }
+};
+
+// extract elements [O, O+VE) of the concatenation (a, b)
+template <int O, typename T, int VE>
+__device__ __forceinline__ Unit<T, VE> extract_at(const Unit<T, VE>& a, const Unit<T, VE>& b) {
+  Unit<T, VE> r;
+#pragma unroll
+  for (int i = 0; i < VE; ++i) r.e[i] = (i + O < VE) ? a.e[i + O] : b.e[i + O - VE];
+  return r;
+}
+template <typename T, int VE>
+__device__ __forceinline__ Unit<T, VE> extract(const Unit<T, VE>& a, const Unit<T, VE>& b, int o) {
+  // o is uniform across the grid (depends only on k*C mod VE)
+  if constexpr (VE == 1) {
+    return a;
+  } else {
+    switch (o) {
+      case 0: return extract_at<0>(a, b);
+      case 1: return extract_at<1>(a, b);
+      default: break;
+    }
+    if constexpr (VE > 2) {
+      switch (o) {
+        case 2: return extract_at<2>(a, b);
+        case 3: return extract_at<3>(a, b);
+        default: break;
+      }
+    }
+    if constexpr (VE > 4) {
+      switch (o) {
+        case 4: return extract_at<4>(a, b);
+        case 5: return extract_at<5>(a, b);
+        case 6: return extract_at<6>(a, b);
+        default: return extract_at<7>(a, b);
+      }
+    }
+    return extract_at<0>(a, b);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// guarded element access: frames < 0 come from the history (the multi-GPU
+// halo / the reference's zero halo, gpu_utils.h:112-123), frames >= nframes
+// and frames before the history read as zero.
+// ----------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T load_elem(const T* __restrict__ in, const T* __restrict__ hist,
+                                       long long f, int c, int C, long long nframes, int k) {
+  if (f >= 0) return f < nframes ? in[f * C + c] : (T)0;
+  if (hist != nullptr && f >= -(long long)(k - 1)) return hist[(f + (k - 1)) * C + c];
+  return (T)0;
+}
+
+// ----------------------------------------------------------------------------
+// streaming scan kernel
+// ----------------------------------------------------------------------------
+struct ScanParams {
+  const void* in;
+  void* out;
+  const void* hist;
+  long long nframes;     // frames in this call
+  long long seg_frames;  // frames per workgroup segment (multiple of chunk frames)
+  int k;                 // window, frames
+  int ring_frames;       // LDS ring size in frames (multiple of chunk frames, >= k + 2*chunk;
+                         // 2*chunk when xkg)
+  int pre_chunks;        // pre-roll chunks per segment (ceil((k-1)/chunk))
+  int xk_off;            // (-k*C) mod VE, elements: offset of x[n-k] inside its aligned unit
+  int xkg;               // 1: read x[n-k] from global memory (k too large for the LDS ring)
+  OutParams o;
+};
+
+// T: sample type; A: accumulator; C: channels; F: frames per lane unit;
+// U: units per lane per chunk; HS: Hillis-Steele flavour.  p.xkg (uniform):
+// read x[n-k] from global memory instead of the LDS ring (very large k).
+template <typename T, typename A, int C, int F, int U, bool HS>
+__global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
+  constexpr int VE = F * C;                 // elements per unit
+  constexpr int CHF = kWG * F * U;          // frames per chunk
+  constexpr int NSEG = U * kNW;             // wave segments per chunk
+  using IO = UnitIO<T, VE>;
+  using U_t = Unit<T, VE>;
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const bool xkg = p.xkg != 0;
+  const int ring_elems = p.ring_frames * C;
+  const int ring_bytes = (ring_elems * (int)sizeof(T) + 15) & ~15;
+  T* ring = reinterpret_cast<T*>(smem);
+  A* tot = reinterpret_cast<A*>(smem + ring_bytes);   // [2][NSEG][C]
+
+  const T* __restrict__ in = static_cast<const T*>(p.in);
+  T* __restrict__ out = static_cast<T*>(p.out);
+  const T* __restrict__ hist = static_cast<const T*>(p.hist);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const long long nframes = p.nframes;
+  const int k = p.k;
+  const int R = p.ring_frames;
+
+  const long long s0 = (long long)blockIdx.x * p.seg_frames;
+  const long long s1 = min(s0 + p.seg_frames, nframes);
+  const long long p0 = s0 - (long long)p.pre_chunks * CHF;
+  const int nch = p.pre_chunks + (int)((s1 - s0 + CHF - 1) / CHF);
+
+  // ---- chunk loader into registers ----------------------------------------
+  auto load_chunk = [&](U_t (&buf)[U], long long c0) {
+    if (c0 >= 0 && c0 + CHF <= nframes) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long f = c0 + (long long)(u * kWG + tid) * F;
+        buf[u] = IO::load(in + f * C);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long f = c0 + (long long)(u * kWG + tid) * F;
+#pragma unroll
+        for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+            buf[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+      }
+    }
+  };
+  auto ring_write = [&](const U_t (&buf)[U], int rpos) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) IO::store(ring + (rpos + (u * kWG + tid) * F) * C, buf[u]);
+  };
+
+  // ---- prologue: zero ring, stage chunk 0, prefetch chunk 1 ----------------
+  {
+    uint4 z = make_uint4(0, 0, 0, 0);
+    for (int i = tid * 16; i < ring_bytes; i += kWG * 16) *reinterpret_cast<uint4*>(smem + i) = z;
+  }
+  U_t buf[U];
+  load_chunk(buf, p0);
+  __syncthreads();
+  ring_write(buf, 0);
+  if (nch > 1) load_chunk(buf, p0 + CHF);
+  __syncthreads();
+
+  A carry[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) carry[c] = (A)0;
+  int rpos = 0;
+
+  for (int ci = 0; ci < nch; ++ci) {
+    const long long c0 = p0 + (long long)ci * CHF;
+    const int par = ci & 1;
+    // ring position (frames) of x[c0 - k]
+    int kb = rpos - k;
+    if (kb < 0) kb += R;
+
+    // (a) d = x - x[n-k], per-lane / per-wave scan, wave-segment totals
+    A v[U][F][C];
+    A lx[U][C];  // lane exclusive prefix inside the wave segment (Blelloch flavour)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = u * kWG + tid;           // unit index in chunk
+      const int q = rpos + j * F;            // ring frame position of this unit
+      U_t x = IO::load(ring + q * C);
+      U_t xk;
+      if (xkg) {
+        // x[n-k] from global memory; frames before the stream start p0 read 0
+        const long long f = c0 + (long long)j * F - k;
+#pragma unroll
+        for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+            xk.e[fr * C + c] = (f + fr < p0) ? (T)0 : load_elem(in, hist, f + fr, c, C, nframes, k);
+      } else if constexpr (IO::kVec) {
+        int qk = kb + j * F;
+        if (qk >= R) qk -= R;
+        if (p.xk_off == 0) {
+          xk = IO::load(ring + qk * C);
+        } else {
+          // x[n-k] straddles two aligned units: read both, shift by xk_off elements
+          const int e_lo = qk * C - p.xk_off;              // aligned unit holding the first element
+          const int e_hi = (e_lo + VE == R * C) ? 0 : e_lo + VE;
+          U_t a = IO::load(ring + e_lo);
+          U_t b = IO::load(ring + e_hi);
+          xk = extract(a, b, p.xk_off);
+        }
+      } else {
+#pragma unroll
+        for (int fr = 0; fr < F; ++fr) {
+          int qf = kb + j * F + fr;
+          if (qf >= R) qf -= R;
+#pragma unroll
+          for (int c = 0; c < C; ++c) xk.e[fr * C + c] = ring[qf * C + c];
+        }
+      }
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          v[u][fr][c] = to_acc<A>(x.e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
+
+      if constexpr (!HS) {
+        // serial in-lane scan, then 64-lane DPP scan of the lane totals
+#pragma unroll
+        for (int fr = 1; fr < F; ++fr)
+#pragma unroll
+          for (int c = 0; c < C; ++c) v[u][fr][c] += v[u][fr - 1][c];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const A t = v[u][F - 1][c];
+          const A incl = wave_incl_scan(t);
+          lx[u][c] = incl - t;
+          const A segtot = readlane(incl, 63);
+          if (lane == 0) tot[(par * NSEG + u * kNW + w) * C + c] = segtot;
+        }
+      } else {
+        // Hillis-Steele over the 64*F frames of the wave segment: every element
+        // adds the element s frames back, s = 1, 2, 4, ..., 32F (log-step, O(n log n)).
+#pragma unroll
+        for (int s = 1; s < F; s <<= 1) {
+          A t[F][C];
+#pragma unroll
+          for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+              if (fr >= s) {
+                t[fr][c] = v[u][fr - s][c];
+              } else {
+                const A nb = shfl_up(v[u][fr - s + F][c], 1);
+                t[fr][c] = lane >= 1 ? nb : (A)0;
+              }
+            }
+#pragma unroll
+          for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[u][fr][c] += t[fr][c];
+        }
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) {
+#pragma unroll
+          for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+              const A nb = shfl_up(v[u][fr][c], m);
+              v[u][fr][c] += lane >= m ? nb : (A)0;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          lx[u][c] = (A)0;
+          const A segtot = readlane(v[u][F - 1][c], 63);
+          if (lane == 0) tot[(par * NSEG + u * kNW + w) * C + c] = segtot;
+        }
+      }
+    }
+
+    // (b) stage chunk ci+1 into the ring, prefetch chunk ci+2
+    int rnext = rpos + CHF;
+    if (rnext == R) rnext = 0;
+    if (ci + 1 < nch) {
+      ring_write(buf, rnext);   // xkg: a 2-chunk ring holding x only
+      if (ci + 2 < nch) load_chunk(buf, c0 + 2LL * CHF);
+    }
+
+    // (c) one barrier per chunk
+    __syncthreads();
+
+    // (d) segment prefixes -> window sums -> outputs
+    A base[U][C];
+    A total[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) total[c] = (A)0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < C; ++c) base[u][c] = carry[c];
+#pragma unroll
+    for (int s = 0; s < NSEG; ++s) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const A t = tot[(par * NSEG + s) * C + c];
+        total[c] += t;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (s < u * kNW + w) base[u][c] += t;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) carry[c] += total[c];
+
+    if (ci >= p.pre_chunks) {
+      const bool full = (c0 + CHF <= s1);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = u * kWG + tid;
+        const long long f = c0 + (long long)j * F;
+        U_t y;
+#pragma unroll
+        for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+            y.e[fr * C + c] = to_out<T, A>(base[u][c] + lx[u][c] + v[u][fr][c], p.o);
+        if (full) {
+          IO::store(out + f * C, y);
+        } else {
+#pragma unroll
+          for (int fr = 0; fr < F; ++fr)
+            if (f + fr < s1)
+#pragma unroll
+              for (int c = 0; c < C; ++c) out[(f + fr) * C + c] = y.e[fr * C + c];
+        }
+      }
+    }
+    rpos = rnext;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// direct LDS-tiled kernel: tile of TF frames + (k-1)-frame halo staged in LDS
+// with VE-element loads; thread t sums the k frames of each output it owns
+// (frames t, t+256, ... of the tile: consecutive lanes read consecutive LDS
+// words, so the O(k) loop is bank-conflict free).
+// ----------------------------------------------------------------------------
+struct DirectParams {
+  const void* in;
+  void* out;
+  const void* hist;
+  long long nframes;
+  int k;
+  int halo_frames;   // roundup(k-1, F)
+  int tile_frames;   // frames per workgroup (multiple of F)
+  OutParams o;
+};
+
+template <typename T, typename A, int C, int F>
+__global__ __launch_bounds__(kWG) void direct_kernel(DirectParams p) {
+  constexpr int VE = F * C;
+  using IO = UnitIO<T, VE>;
+  using U_t = Unit<T, VE>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* tile = reinterpret_cast<T*>(smem);
+
+  const T* __restrict__ in = static_cast<const T*>(p.in);
+  T* __restrict__ out = static_cast<T*>(p.out);
+  const T* __restrict__ hist = static_cast<const T*>(p.hist);
+  const int tid = threadIdx.x;
+  const int k = p.k;
+  const long long nframes = p.nframes;
+  const long long t0 = (long long)blockIdx.x * p.tile_frames;
+  const long long a0 = t0 - p.halo_frames;            // first staged frame
+  const int nunits = (p.halo_frames + p.tile_frames) / F;
+
+  const bool fast = (a0 >= 0) && (t0 + p.tile_frames <= nframes);
+  for (int j = tid; j < nunits; j += kWG) {
+    const long long f = a0 + (long long)j * F;
+    U_t u;
+    if (fast) {
+      u = IO::load(in + f * C);
+    } else {
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c) u.e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+    }
+    IO::store(tile + j * VE, u);
+  }
+  __syncthreads();
+
+  const long long tend = min(t0 + (long long)p.tile_frames, nframes);
+  for (int i = tid; i < p.tile_frames; i += kWG) {
+    const long long f = t0 + i;
+    if (f >= tend) break;
+    const int lf = p.halo_frames + i;  // tile-local frame
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      A s = (A)0;
+      const T* src = tile + lf * C + c;
+      for (int j = 0; j < k; ++j) s += to_acc<A>(src[-j * C]);
+      out[f * C + c] = to_out<T, A>(s, p.o);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// naive kernel: one thread per sample, k reads from global memory
+// (profilable_parallel_averager.cu:14-23, with the history contract instead
+// of reading before the buffer).
+// ----------------------------------------------------------------------------
+template <typename T, typename A>
+__global__ __launch_bounds__(kWG) void naive_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                    const T* __restrict__ hist, long long nframes,
+                                                    int C, int k, OutParams o) {
+  const long long idx = (long long)blockIdx.x * kWG + threadIdx.x;
+  const long long n = nframes * C;
+  if (idx >= n) return;
+  const long long f = idx / C;
+  const int c = (int)(idx - f * C);
+  A s = (A)0;
+  for (int j = 0; j < k; ++j) s += to_acc<A>(load_elem(in, hist, f - j, c, C, nframes, k));
+  out[idx] = to_out<T, A>(s, o);
+}
+
+// ----------------------------------------------------------------------------
+// synthetic input: identical to oracle/mavg_oracle.c (oracle_synth_*)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kWG) void synth_kernel(T* __restrict__ out, long long n, uint64_t base, int dist) {
+  const long long stride = (long long)gridDim.x * kWG;
+  for (long long i = (long long)blockIdx.x * kWG + threadIdx.x; i < n; i += stride) {
+    const uint64_t h = splitmix64(base + (uint64_t)i);
+    if constexpr (sizeof(T) == 2) {
+      out[i] = (T)(int16_t)(uint16_t)(h >> 48);
+    } else {
+      out[i] = dist == 1 ? (float)(h >> 40) * (1.0f / 16777216.0f) : (float)(int16_t)(uint16_t)(h >> 48);
+    }
+  }
+}
+
+}  // namespace mavg

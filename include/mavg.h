@@ -1,0 +1,116 @@
+/*
+ * mavg.h -- C ABI of libmavg, the MI355X-native (gfx950) causal moving-average
+ * filter.  Plain pointers and sizes only; no HIP, torch or C++ types.
+ *
+ * This is the in-process replacement for the reference's per-variant
+ * "<Variant>GpuLoad" drivers and their kernels:
+ *
+ *   reference                                              replaced by
+ *   ---------------------------------------------------    -------------------------
+ *   blellochAveragerGpuLoad  basics/blelloch_scan_averager.cu:189-232        mavg_run(.., MAVG_ALGO_BLELLOCH_SCALAR ..)
+ *     recursive_blelloch :134-167, blelloch_scan_inclusive :40-131,
+ *     blelloch_uniform_add :17-36, averager_kernel :171-186
+ *   blellochAveragerGpuLoad  basics/blelloch_scan_vloaded_averager.cu:183-228 mavg_run(.., MAVG_ALGO_BLELLOCH ..)
+ *   hillisSteeleAveragerGpuLoad basics/hillis_steele_averager.cu:221-249     mavg_run(.., MAVG_ALGO_HILLIS_SCALAR ..)
+ *   (vloaded)                basics/hillis_steele_vloaded_averager.cu         mavg_run(.., MAVG_ALGO_HILLIS ..)
+ *   vload4AveragerGpuLoad    basics/profilable_sm_vload4.cu:91-145            mavg_run(.., MAVG_ALGO_DIRECT ..)
+ *   vload2AveragerGpuLoad    basics/profilable_sm_vload2.cu:65-92             mavg_run(.., MAVG_ALGO_DIRECT_VEC2 ..)
+ *   sharedMemoryAveragerGpuLoad basics/profilable_sm_averager.cu:48-74       mavg_run(.., MAVG_ALGO_DIRECT_SCALAR ..)
+ *   parallelAveragerGpuLoad  basics/profilable_parallel_averager.cu:26-51    mavg_run(.., MAVG_ALGO_NAIVE ..)
+ *   DspWorkspace<T,Mode>     gpu_utils.h:67-160 (halo zone, scratch)         caller-owned buffers + d_history
+ *                                                                             + mavg_workspace_bytes
+ *
+ * Semantics (all algorithms, both dtypes) follow the serial reference
+ * basics/profilable_moving_averager.cpp:14-37: interleaved frames x[f*C + c],
+ * window k ("grade"), frames before the first one read as zero -- or, when
+ * d_history is given, as the (k-1)*C samples immediately preceding d_in
+ * (the multi-GPU halo; gpu_utils.h:112-123 is the reference's zero halo).
+ *   MAVG_I16: y = (int16)(S / k), S the exact int64 window sum, C++ truncating
+ *             division.  Bit-exact with the serial reference (the reference's
+ *             GPU variants use a float reciprocal and are not).
+ *   MAVG_F32: y = (float)(S / k), S accumulated in fp64; within 1e-5 relative
+ *             of the fp64 serial restatement.
+ *
+ * Ownership: the caller owns d_in, d_out, d_history and d_ws (device memory);
+ * mavg_run never allocates, never synchronises, never exits, and only
+ * enqueues work on `stream` (a hipStream_t; NULL = the legacy default
+ * stream), so it can be captured into a HIP graph.  d_in is const (the
+ * reference scans in place; this library does not).  Re-entrant, no globals
+ * other than a per-device attribute cache.
+ */
+#ifndef MAVG_H
+#define MAVG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAVG_ABI_VERSION 1
+
+typedef enum {
+    MAVG_I16 = 0, /* int16 PCM in/out (the reference's WAV data path) */
+    MAVG_F32 = 1  /* fp32 in/out (BASELINE.json north_star) */
+} mavg_dtype;
+
+typedef enum {
+    MAVG_ALGO_AUTO = 0,            /* pick by (dtype, k, C): see DESIGN.md */
+    MAVG_ALGO_BLELLOCH = 1,        /* single-pass streaming work-efficient scan, 16-B units */
+    MAVG_ALGO_BLELLOCH_SCALAR = 2, /* same scan, one frame per lane */
+    MAVG_ALGO_HILLIS = 3,          /* streaming Hillis-Steele (log-step) scan, 16-B units */
+    MAVG_ALGO_HILLIS_SCALAR = 4,   /* Hillis-Steele, one frame per lane */
+    MAVG_ALGO_DIRECT = 5,          /* direct LDS-tiled window sum, 16-B loads (vload4) */
+    MAVG_ALGO_DIRECT_VEC2 = 6,     /* direct LDS-tiled, 8-B loads (vload2) */
+    MAVG_ALGO_DIRECT_SCALAR = 7,   /* direct LDS-tiled, element loads (shared) */
+    MAVG_ALGO_NAIVE = 8            /* one thread per sample, window from global memory */
+} mavg_algo;
+
+typedef enum {
+    MAVG_OK = 0,
+    MAVG_ERR_INVALID_ARG = 1, /* null pointer, k < 1, C < 1, n not a multiple of C, bad enum */
+    MAVG_ERR_UNSUPPORTED = 2, /* valid but not implemented (e.g. C > 8, k too large for algo) */
+    MAVG_ERR_MISALIGNED = 3,  /* a 16-B-unit algorithm got a pointer not 16-B aligned */
+    MAVG_ERR_WORKSPACE = 4,   /* ws_bytes smaller than mavg_workspace_bytes() */
+    MAVG_ERR_HIP = 5          /* a HIP runtime call or kernel launch failed */
+} mavg_status;
+
+/* Device workspace (bytes) mavg_run needs for this problem; 0 is valid. */
+int mavg_workspace_bytes(size_t n_samples, int channels, int grade, int dtype,
+                         int algo, int block_size, size_t* out_bytes);
+
+/*
+ * y[0..n) = moving average of x[0..n), n = frames * channels samples.
+ *   d_history  NULL (zero history) or (grade-1)*channels samples that
+ *              precede d_in (any alignment).
+ *   block_size the reference's argv block size (multiple of 32 in
+ *              [32, 1024]); kernels use it rounded up to a multiple of the
+ *              64-lane wavefront where the algorithm takes a block size,
+ *              0 = the algorithm's tuned default.
+ *   stream     hipStream_t or NULL.
+ * Returns a mavg_status.  Nothing is enqueued unless MAVG_OK is returned
+ * (MAVG_ERR_HIP excepted, when the launch itself failed).
+ */
+int mavg_run(const void* d_in, void* d_out, size_t n_samples, int channels,
+             int grade, int dtype, int algo, int block_size,
+             const void* d_history, void* d_ws, size_t ws_bytes, void* stream);
+
+/* The algorithm MAVG_ALGO_AUTO resolves to for these arguments. */
+int mavg_resolve_algo(size_t n_samples, int channels, int grade, int dtype, int algo);
+
+/* Counter-based synthetic signal on the device: x[i] for global index
+ * offset+i, from splitmix64(seed + offset + i).  dist 0: int16-valued
+ * (as int16 or as float); dist 1: uniform [0,1) floats (MAVG_F32 only). */
+int mavg_fill_synthetic(void* d_out, size_t n_samples, int dtype, uint64_t seed,
+                        uint64_t offset, int dist, void* stream);
+
+const char* mavg_strerror(int status);
+const char* mavg_algo_name(int algo);
+int mavg_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MAVG_H */

@@ -1,0 +1,124 @@
+"""CPU oracle for the moving-average hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this package, and only as the checker or as the timed CPU
+baseline.  The product (``digital_signal_processsing_amd``, ``libmavg.so``,
+the ``bin_*`` CLIs) never imports it.
+
+Parity status: **unpinned** against an executed reference -- the reference's
+CPU averager does not compile as shipped and the reference holds no golden
+vectors (see ``mavg_oracle.c`` header and DESIGN.md).  The C restatement
+(``oracle_mavg_*``, following ``basics/profilable_moving_averager.cpp:14-37``)
+is cross-checked against the independent numpy formulation below and against
+closed-form known answers in ``tests/test_oracle.py``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    """Compile the C restatement (gcc) into oracle/liboracle.so."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def _load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        build()
+    lib = ctypes.CDLL(_LIB_PATH)
+    p, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+    lib.oracle_mavg_i16.argtypes = [p, p, sz, i, i]
+    lib.oracle_mavg_f32.argtypes = [p, p, sz, i, i]
+    lib.oracle_window_sum_i64.argtypes = [p, sz, i, i, sz, sz, p]
+    lib.oracle_synth_i16.argtypes = [p, sz, u64, u64]
+    lib.oracle_synth_f32.argtypes = [p, sz, u64, u64, i]
+    for f in (lib.oracle_mavg_i16, lib.oracle_mavg_f32, lib.oracle_window_sum_i64):
+        f.restype = ctypes.c_int
+    lib.oracle_synth_i16.restype = None
+    lib.oracle_synth_f32.restype = None
+    _lib = lib
+    return lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def mavg_i16(x: np.ndarray, k: int, channels: int = 1) -> np.ndarray:
+    """int16 mode, bit-exact restatement of profilable_cpu_computations."""
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    y = np.zeros_like(x)
+    rc = _load().oracle_mavg_i16(_ptr(x), _ptr(y), x.size, channels, k)
+    if rc != 0:
+        raise ValueError(f"oracle_mavg_i16: bad arguments (n={x.size}, C={channels}, k={k})")
+    return y
+
+
+def mavg_f32(x: np.ndarray, k: int, channels: int = 1) -> np.ndarray:
+    """fp32 mode: double running sum, float(sum / k)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.zeros_like(x)
+    rc = _load().oracle_mavg_f32(_ptr(x), _ptr(y), x.size, channels, k)
+    if rc != 0:
+        raise ValueError(f"oracle_mavg_f32: bad arguments (n={x.size}, C={channels}, k={k})")
+    return y
+
+
+def window_sum_i64(x: np.ndarray, k: int, channels: int, f0: int, f1: int) -> np.ndarray:
+    """Exact int64 windowed sums for frames [f0, f1) (zero history)."""
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    out = np.zeros((f1 - f0) * channels, dtype=np.int64)
+    rc = _load().oracle_window_sum_i64(_ptr(x), x.size, channels, k, f0, f1, _ptr(out))
+    if rc != 0:
+        raise ValueError("oracle_window_sum_i64: bad arguments")
+    return out
+
+
+def synth_i16(n: int, seed: int = 0x5EED, offset: int = 0) -> np.ndarray:
+    x = np.empty(n, dtype=np.int16)
+    _load().oracle_synth_i16(_ptr(x), n, seed, offset)
+    return x
+
+
+def synth_f32(n: int, seed: int = 0x5EED, offset: int = 0, dist: int = 0) -> np.ndarray:
+    x = np.empty(n, dtype=np.float32)
+    _load().oracle_synth_f32(_ptr(x), n, seed, offset, dist)
+    return x
+
+
+# ---------------------------------------------------------------------------
+# Independent numpy formulation (per-channel prefix sums).  Used only to
+# cross-check the C restatement; it shares no code with it.
+# ---------------------------------------------------------------------------
+def numpy_window_sum(x: np.ndarray, k: int, channels: int = 1) -> np.ndarray:
+    """S[f, c] = sum_{j<k} x[(f-j)C + c] with zero history, exact in int64 /
+    float64 (float64 only approximately for non-integer float data)."""
+    xf = x.reshape(-1, channels)
+    acc = np.int64 if np.issubdtype(x.dtype, np.integer) else np.float64
+    p = np.cumsum(xf.astype(acc), axis=0)
+    s = p.copy()
+    if k < p.shape[0]:
+        s[k:] = p[k:] - p[:-k]
+    return s.reshape(-1)
+
+
+def numpy_mavg_i16(x: np.ndarray, k: int, channels: int = 1) -> np.ndarray:
+    s = numpy_window_sum(x.astype(np.int16), k, channels)
+    q = np.abs(s) // k  # C++ integer division truncates toward zero
+    return (np.sign(s) * q).astype(np.int16)
+
+
+def numpy_mavg_f32(x: np.ndarray, k: int, channels: int = 1) -> np.ndarray:
+    return (numpy_window_sum(x.astype(np.float32), k, channels) / float(k)).astype(np.float32)

@@ -1,0 +1,133 @@
+/*
+ * mavg_oracle.c -- CPU restatement of the reference moving-average filter.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (libmavg, the bin_* CLIs,
+ * the Python package) links, loads or calls this file.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg use it, and only
+ * as the checker / the timed CPU baseline.
+ *
+ * PARITY STATUS: unpinned against an executed reference.  The reference's own
+ * CPU averager (basics/profilable_moving_averager.cpp) does not compile as
+ * shipped (no closing brace after :83; benchmark.h:5 and gpu_utils.h:2
+ * include <cuda_runtime.h>, absent here) and the reference holds no tests,
+ * golden vectors or fixtures.  This restatement follows
+ * the reference loop statement by statement and is cross-checked against an
+ * independent numpy formulation and closed-form known answers in tests/.
+ *
+ * Semantics (basics/profilable_moving_averager.cpp:14-37):
+ *   samples are interleaved frames x[f*C + c]; window length k ("point");
+ *   per channel a running int64 sum; warm-up loop :19-25 adds frames 0..k-1
+ *   and divides by k (not by the number of frames seen); steady loop :27-35
+ *   subtracts frame f-k then adds frame f; output = (int16)(sum / k) with
+ *   C++ truncating int64 division.
+ *
+ * fp32 mode (BASELINE.json north_star): the same loop with a double running
+ * sum over float inputs and output (float)(sum / k) -- SURVEY.md section 8c.
+ */
+#include <stdint.h>
+#include <stddef.h>
+#include <string.h>
+#include <stdlib.h>
+
+#define ORACLE_MAX_CH 64
+
+/* Follows profilable_moving_averager.cpp:14-37.  Returns 0, or -1 on bad args.
+ * Deviation (documented): the warm-up loop is clamped to the frame count; the
+ * reference reads past the end when k > frames (:19-23, undefined behaviour). */
+int oracle_mavg_i16(const int16_t* x, int16_t* y, size_t n, int C, int k)
+{
+    if (C < 1 || C > ORACLE_MAX_CH || k < 1 || (n % (size_t)C) != 0) return -1;
+    const size_t frames = n / (size_t)C;                 /* :16 */
+    int64_t sum[ORACLE_MAX_CH];                          /* :17 */
+    memset(sum, 0, sizeof(sum));
+    const size_t warm = (size_t)k < frames ? (size_t)k : frames;
+    for (size_t i = 0; i < warm; ++i) {                  /* :19 */
+        for (int ch = 0; ch < C; ++ch) {                 /* :20 */
+            sum[ch] += x[i * C + ch];                    /* :21-22 */
+            y[i * C + ch] = (int16_t)(sum[ch] / k);      /* :23 */
+        }
+    }
+    for (size_t i = (size_t)k; i < frames; ++i) {        /* :27 */
+        for (int ch = 0; ch < C; ++ch) {                 /* :28 */
+            sum[ch] -= x[(i - (size_t)k) * C + ch];      /* :30-31 */
+            sum[ch] += x[i * C + ch];                    /* :29,32 */
+            y[i * C + ch] = (int16_t)(sum[ch] / k);      /* :33 */
+        }
+    }
+    return 0;
+}
+
+/* fp32 mode: same loop structure, double running sum, float(sum / k). */
+int oracle_mavg_f32(const float* x, float* y, size_t n, int C, int k)
+{
+    if (C < 1 || C > ORACLE_MAX_CH || k < 1 || (n % (size_t)C) != 0) return -1;
+    const size_t frames = n / (size_t)C;
+    double sum[ORACLE_MAX_CH];
+    for (int ch = 0; ch < C; ++ch) sum[ch] = 0.0;
+    const double dk = (double)k;
+    const size_t warm = (size_t)k < frames ? (size_t)k : frames;
+    for (size_t i = 0; i < warm; ++i)
+        for (int ch = 0; ch < C; ++ch) {
+            sum[ch] += (double)x[i * C + ch];
+            y[i * C + ch] = (float)(sum[ch] / dk);
+        }
+    for (size_t i = (size_t)k; i < frames; ++i)
+        for (int ch = 0; ch < C; ++ch) {
+            sum[ch] -= (double)x[(i - (size_t)k) * C + ch];
+            sum[ch] += (double)x[i * C + ch];
+            y[i * C + ch] = (float)(sum[ch] / dk);
+        }
+    return 0;
+}
+
+/* Exact windowed sums (int64) for a sub-range of frames [f0, f1) of a signal
+ * whose frames before 0 are zero: used by tests to check arbitrary slices
+ * (e.g. shard boundaries) of a long signal without running the whole loop. */
+int oracle_window_sum_i64(const int16_t* x, size_t n, int C, int k,
+                          size_t f0, size_t f1, int64_t* out)
+{
+    if (C < 1 || C > ORACLE_MAX_CH || k < 1 || (n % (size_t)C) != 0) return -1;
+    const size_t frames = n / (size_t)C;
+    if (f1 > frames || f0 > f1) return -1;
+    for (int ch = 0; ch < C; ++ch) {
+        int64_t s = 0;
+        size_t lo = f0 + 1 > (size_t)k ? f0 + 1 - (size_t)k : 0;
+        for (size_t j = lo; j <= f0 && f0 < f1; ++j) s += x[j * C + ch];
+        for (size_t f = f0; f < f1; ++f) {
+            if (f > f0) {
+                s += x[f * C + ch];
+                if (f >= (size_t)k) s -= x[(f - (size_t)k) * C + ch];
+            }
+            out[(f - f0) * C + ch] = s;
+        }
+    }
+    return 0;
+}
+
+/* ---- counter-based synthetic input ----------------------
+ * x[i] = (int16)(splitmix64(seed + i) >> 48); the GPU generator in
+ * libmavg computes the identical sequence so any sub-range can be regenerated
+ * on the host.  dist 0: int16-valued; dist 1: uniform [0,1) with 24-bit
+ * mantissa (precision stress, parity tests only). */
+static inline uint64_t splitmix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+void oracle_synth_i16(int16_t* x, size_t n, uint64_t seed, uint64_t offset)
+{
+    for (size_t i = 0; i < n; ++i)
+        x[i] = (int16_t)(uint16_t)(splitmix64(seed + offset + i) >> 48);
+}
+
+void oracle_synth_f32(float* x, size_t n, uint64_t seed, uint64_t offset, int dist)
+{
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t h = splitmix64(seed + offset + i);
+        if (dist == 1) x[i] = (float)(h >> 40) * (1.0f / 16777216.0f);
+        else           x[i] = (float)(int16_t)(uint16_t)(h >> 48);
+    }
+}

@@ -1,0 +1,191 @@
+"""GPU parity: libmavg (HIP, gfx950) against the CPU oracle on the same seeded
+inputs.  int16 results must be bit-exact with the serial reference semantics
+(basics/profilable_moving_averager.cpp:14-37); fp32 results must be within
+RTOL relative of the fp64 restatement (BASELINE.json north_star: 1e-5)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5  # north_star: "within 1e-5 relative fp32"
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+ALL_ALGOS = ["blelloch", "blelloch_scalar", "hillis", "hillis_scalar", "direct", "direct_vec2",
+             "direct_scalar", "naive"]
+
+
+def _dev(x, gpu):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x)).to(gpu)
+
+
+def _run(x_np, k, C, algo, gpu, history=None):
+    import digital_signal_processsing_amd as dsp
+    x = _dev(x_np, gpu)
+    h = _dev(history, gpu) if history is not None else None
+    y = dsp.moving_average(x, k, channels=C, algo=algo, history=h)
+    return y.cpu().numpy()
+
+
+def assert_f32_close(y, r, what=""):
+    err = np.abs(y.astype(np.float64) - r.astype(np.float64))
+    tol = RTOL * np.maximum(np.abs(r.astype(np.float64)), 1e-30)
+    bad = np.nonzero(err > tol)[0]
+    assert bad.size == 0, f"{what}: {bad.size} mismatches, first at {bad[:5]}: got {y[bad[:5]]} want {r[bad[:5]]}"
+
+
+# ---------------------------------------------------------------------------
+def test_device_synth_matches_oracle(oracle_mod, gpu):
+    import digital_signal_processsing_amd as dsp
+    import torch
+    n = 100_003
+    for dist in (0, 1):
+        y = dsp.fill_synthetic(n, torch.float32, seed=0x5EED, offset=999, dist=dist, device=gpu)
+        assert np.array_equal(y.cpu().numpy(), oracle_mod.synth_f32(n, seed=0x5EED, offset=999, dist=dist))
+    y = dsp.fill_synthetic(n, torch.int16, seed=7, offset=3, device=gpu)
+    assert np.array_equal(y.cpu().numpy(), oracle_mod.synth_i16(n, seed=7, offset=3))
+
+
+@pytest.mark.parametrize("algo", ALL_ALGOS)
+@pytest.mark.parametrize("C", [1, 2])
+def test_golden_fixtures_i16(oracle_mod, gpu, algo, C):
+    g = np.load(os.path.join(GOLDEN, "mavg_golden.npz"))
+    x = oracle_mod.synth_i16(4096 * C, seed=0x5EED)
+    for k in (1, 3, 7, 32, 41, 64, 1000, 1024):
+        y = _run(x, k, C, algo, gpu)
+        assert np.array_equal(y, g[f"i16_C{C}_k{k}"]), f"{algo} C={C} k={k}"
+
+
+@pytest.mark.parametrize("algo", ALL_ALGOS)
+@pytest.mark.parametrize("C", [1, 2])
+def test_golden_fixtures_f32(oracle_mod, gpu, algo, C):
+    g = np.load(os.path.join(GOLDEN, "mavg_golden.npz"))
+    x = oracle_mod.synth_f32(4096 * C, seed=0x5EED, dist=1)
+    for k in (1, 3, 7, 32, 41, 64, 1000, 1024):
+        assert_f32_close(_run(x, k, C, algo, gpu), g[f"f32u_C{C}_k{k}"], f"{algo} C={C} k={k}")
+
+
+# sizes: tiny, ragged (not multiples of any chunk / vector), multi-segment
+SIZES = [1, 5, 63, 1000, 4097, 65_537, 1_000_003]
+SCAN_ALGOS = ["blelloch", "blelloch_scalar", "hillis", "hillis_scalar"]
+
+
+@pytest.mark.parametrize("algo", SCAN_ALGOS + ["direct", "naive"])
+@pytest.mark.parametrize("frames", SIZES)
+def test_ragged_sizes_i16(oracle_mod, gpu, algo, frames):
+    for C, k in ((1, 1), (1, 7), (1, 1024), (2, 64), (2, 41)):
+        if algo == "naive" and frames * k > 50_000_000:
+            continue
+        x = oracle_mod.synth_i16(frames * C, offset=frames + k)
+        y = _run(x, k, C, algo, gpu)
+        assert np.array_equal(y, oracle_mod.mavg_i16(x, k, C)), f"{algo} frames={frames} C={C} k={k}"
+
+
+@pytest.mark.parametrize("algo", SCAN_ALGOS + ["direct"])
+@pytest.mark.parametrize("frames", SIZES)
+def test_ragged_sizes_f32(oracle_mod, gpu, algo, frames):
+    for C, k, dist in ((1, 1, 0), (1, 7, 1), (1, 1024, 0), (1, 4096, 1), (2, 64, 1), (4, 3, 0)):
+        x = oracle_mod.synth_f32(frames * C, offset=frames + k, dist=dist)
+        assert_f32_close(_run(x, k, C, algo, gpu), oracle_mod.mavg_f32(x, k, C),
+                         f"{algo} frames={frames} C={C} k={k} dist={dist}")
+
+
+@pytest.mark.parametrize("C", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("dtype", ["i16", "f32"])
+def test_all_channel_counts(oracle_mod, gpu, C, dtype):
+    frames = 20_011
+    for algo in ("blelloch", "hillis_scalar", "direct", "naive"):
+        for k in (1, 5, 333):
+            if dtype == "i16":
+                x = oracle_mod.synth_i16(frames * C, offset=C * 1000 + k)
+                assert np.array_equal(_run(x, k, C, algo, gpu), oracle_mod.mavg_i16(x, k, C)), (algo, C, k)
+            else:
+                x = oracle_mod.synth_f32(frames * C, offset=C * 1000 + k, dist=1)
+                assert_f32_close(_run(x, k, C, algo, gpu), oracle_mod.mavg_f32(x, k, C), f"{algo} C={C} k={k}")
+
+
+@pytest.mark.parametrize("k", [2, 3, 5, 6, 7, 9, 13, 4093, 4097, 20_000, 70_000])
+def test_unaligned_and_large_windows(oracle_mod, gpu, k):
+    """x[n-k] not 16-B aligned inside the LDS ring; k too large for the ring
+    (global re-read path); int16 k > 65535 (int64 accumulation)."""
+    frames = 300_007
+    for C in (1, 2):
+        x = oracle_mod.synth_i16(frames * C, offset=k)
+        for algo in ("blelloch", "hillis"):
+            assert np.array_equal(_run(x, k, C, algo, gpu), oracle_mod.mavg_i16(x, k, C)), (algo, C, k)
+        xf = oracle_mod.synth_f32(frames * C, offset=k, dist=1)
+        assert_f32_close(_run(xf, k, C, "blelloch", gpu), oracle_mod.mavg_f32(xf, k, C), f"C={C} k={k}")
+
+
+@pytest.mark.parametrize("algo", ["blelloch", "blelloch_scalar", "hillis", "direct", "direct_scalar", "naive"])
+@pytest.mark.parametrize("dtype", ["i16", "f32"])
+def test_history_equals_concatenation(oracle_mod, gpu, algo, dtype):
+    """Sharding contract: running on x[a:] with the (k-1)*C preceding samples
+    as history equals the tail of running on the whole signal."""
+    C, k, frames, cut = 2, 300, 50_000, 17_001
+    if dtype == "i16":
+        x = oracle_mod.synth_i16(frames * C, offset=11)
+        full = oracle_mod.mavg_i16(x, k, C)
+    else:
+        x = oracle_mod.synth_f32(frames * C, offset=11, dist=1)
+        full = oracle_mod.mavg_f32(x, k, C)
+    hist = x[(cut - (k - 1)) * C: cut * C]
+    y = _run(x[cut * C:], k, C, algo, gpu, history=hist)
+    if dtype == "i16":
+        assert np.array_equal(y, full[cut * C:])
+    else:
+        assert_f32_close(y, full[cut * C:], algo)
+
+
+def test_properties_identity_constant_linearity(oracle_mod, gpu):
+    import digital_signal_processsing_amd as dsp
+    import torch
+    n = 1 << 20
+    x = dsp.fill_synthetic(n, torch.int16, seed=3, device=gpu)
+    assert torch.equal(dsp.moving_average(x, 1), x)                                  # k=1 identity
+    c = torch.full((n,), -1234, dtype=torch.int16, device=gpu)
+    y = dsp.moving_average(c, 777)
+    assert (y[776:] == -1234).all()                                                   # constant from k-1 on
+    a = dsp.fill_synthetic(n, torch.float32, seed=4, device=gpu)
+    b = dsp.fill_synthetic(n, torch.float32, seed=5, device=gpu)
+    ya, yb, yab = dsp.moving_average(a, 100), dsp.moving_average(b, 100), dsp.moving_average(a + 2 * b, 100)
+    torch.testing.assert_close(yab, ya + 2 * yb, rtol=1e-5, atol=1e-3)               # linearity
+
+
+def test_full_size_headline_config(oracle_mod, gpu):
+    """BASELINE.json headline config (N=2^30 fp32, k=1024): int16-valued input
+    makes every window sum exact, so each checked output must equal the oracle
+    to <= 1 ulp; checked at every workgroup-segment and chunk boundary region
+    and at random positions."""
+    import digital_signal_processsing_amd as dsp
+    import torch
+    n, k, seed = 1 << 30, 1024, 0x5EED
+    x = dsp.fill_synthetic(n, torch.float32, seed=seed, device=gpu)
+    y = dsp.moving_average(x, k, algo="blelloch")
+    del x
+    rng = np.random.default_rng(0)
+    starts = list(rng.integers(0, n - 4096, 200)) + [0, n - 4096]
+    # boundaries of every 2^16-frame block (covers segment + chunk edges at any tuning)
+    starts += list(range((1 << 16) - 2048, n - 4096, 1 << 21))
+    ycpu = y.cpu().numpy()
+    for s in starts:
+        s = int(s)
+        a = max(0, s - k + 1)
+        xs = oracle_mod.synth_f32(s + 4096 - a, seed=seed, offset=a)
+        ref = oracle_mod.mavg_f32(xs, k, 1)[s - a:]
+        assert_f32_close(ycpu[s:s + 4096], ref, f"slice at {s}")
+
+
+def test_checksum_of_checksums_repeatability(gpu):
+    """Same input, repeated launches: the output is deterministic bit-for-bit."""
+    import digital_signal_processsing_amd as dsp
+    import torch
+    x = dsp.fill_synthetic(1 << 26, torch.float32, seed=9, device=gpu)
+    h = None
+    for _ in range(3):
+        y = dsp.moving_average(x, 64)
+        d = torch.sum(y.view(torch.int32).to(torch.int64) * 2654435761 % (1 << 31)).item()
+        assert h is None or d == h
+        h = d

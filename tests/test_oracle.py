@@ -1,0 +1,107 @@
+"""CPU tests of the oracle (the checker): C restatement vs an independent numpy
+formulation, closed-form known answers derived from the reference loop
+(basics/profilable_moving_averager.cpp:14-37), and the committed fixtures."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("C", [1, 2, 3, 8])
+@pytest.mark.parametrize("k", [1, 2, 3, 7, 32, 41, 64, 1000, 4096, 5000])
+def test_c_restatement_matches_numpy_i16(oracle_mod, C, k):
+    x = oracle_mod.synth_i16(3000 * C, offset=17 * C + k)
+    assert np.array_equal(oracle_mod.mavg_i16(x, k, C), oracle_mod.numpy_mavg_i16(x, k, C))
+
+
+@pytest.mark.parametrize("C", [1, 2, 5])
+@pytest.mark.parametrize("k", [1, 7, 64, 1024])
+@pytest.mark.parametrize("dist", [0, 1])
+def test_c_restatement_matches_numpy_f32(oracle_mod, C, k, dist):
+    x = oracle_mod.synth_f32(3000 * C, offset=5, dist=dist)
+    a = oracle_mod.mavg_f32(x, k, C)
+    b = oracle_mod.numpy_mavg_f32(x, k, C)
+    np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6 * np.abs(b).max())
+
+
+def test_known_answers_i16(oracle_mod):
+    # constant input c: warm-up frames f < k give (c*(f+1))/k truncated; then c
+    k, c = 5, 7
+    y = oracle_mod.mavg_i16(np.full(20, c, np.int16), k)
+    assert list(y[:5]) == [(c * (f + 1)) // k for f in range(5)]
+    assert (y[4:] == c).all()
+    # impulse: y = trunc(A / k) for k frames after the impulse, else 0
+    x = np.zeros(30, np.int16)
+    x[10] = 1000
+    y = oracle_mod.mavg_i16(x, 7)
+    assert (y[10:17] == 1000 // 7).all() and (y[:10] == 0).all() and (y[17:] == 0).all()
+    # negative sums truncate toward zero (C++ int64 division), not floor
+    x = np.array([-7, 0, 0, -1], np.int16)
+    assert list(oracle_mod.mavg_i16(x, 2)) == [-3, -3, 0, 0]
+    # k = 1 is the identity
+    x = oracle_mod.synth_i16(1000)
+    assert np.array_equal(oracle_mod.mavg_i16(x, 1), x)
+    # stereo channels are independent
+    x = np.zeros(20, np.int16)
+    x[0::2] = 4
+    x[1::2] = -8
+    y = oracle_mod.mavg_i16(x, 2, 2)
+    assert list(y[:4]) == [2, -4, 4, -8]
+
+
+def test_known_answers_f32(oracle_mod):
+    x = np.arange(1, 11, dtype=np.float32)
+    y = oracle_mod.mavg_f32(x, 4)
+    # frame i holds i+1; warm-up divides by k even before k frames were seen
+    sums = [1, 3, 6, 10] + [(i - 2) + (i - 1) + i + (i + 1) for i in range(4, 10)]
+    expect = np.array([s / 4 for s in sums], np.float32)
+    np.testing.assert_array_equal(y, expect)
+
+
+def test_window_sum_slices(oracle_mod):
+    x = oracle_mod.synth_i16(10000 * 2, offset=3)
+    full = oracle_mod.numpy_window_sum(x, 300, 2)
+    for f0, f1 in [(0, 10), (299, 301), (4000, 6000), (9990, 10000)]:
+        got = oracle_mod.window_sum_i64(x, 300, 2, f0, f1)
+        assert np.array_equal(got, full[f0 * 2:f1 * 2])
+
+
+def test_synth_matches_spec(oracle_mod):
+    # splitmix64 reference values computed independently in Python
+    def splitmix64(z):
+        m = (1 << 64) - 1
+        z = (z + 0x9E3779B97F4A7C15) & m
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+        return z ^ (z >> 31)
+
+    seed, off = 0x5EED, 123
+    x = oracle_mod.synth_i16(64, seed=seed, offset=off)
+    xf = oracle_mod.synth_f32(64, seed=seed, offset=off, dist=1)
+    for i in range(64):
+        h = splitmix64(seed + off + i)
+        assert int(x[i]) == np.int16(np.uint16(h >> 48))
+        assert float(xf[i]) == np.float32((h >> 40) / 16777216.0)
+
+
+def test_invalid_args(oracle_mod):
+    with pytest.raises(ValueError):
+        oracle_mod.mavg_i16(np.zeros(5, np.int16), 2, 2)  # n not a multiple of C
+    with pytest.raises(ValueError):
+        oracle_mod.mavg_i16(np.zeros(4, np.int16), 0, 1)  # k < 1
+
+
+def test_golden_fixtures(oracle_mod):
+    g = np.load(os.path.join(GOLDEN, "mavg_golden.npz"))
+    for C in (1, 2):
+        x = oracle_mod.synth_i16(4096 * C, seed=0x5EED)
+        xf = oracle_mod.synth_f32(4096 * C, seed=0x5EED, dist=1)
+        for k in (1, 3, 7, 32, 41, 64, 1000, 1024):
+            assert np.array_equal(oracle_mod.mavg_i16(x, k, C), g[f"i16_C{C}_k{k}"])
+            assert np.array_equal(oracle_mod.mavg_f32(xf, k, C), g[f"f32u_C{C}_k{k}"])
+    digests = dict(line.split() for line in open(os.path.join(GOLDEN, "digests.txt")))
+    x = oracle_mod.synth_i16(1 << 20, seed=0x5EED)
+    assert hashlib.sha256(oracle_mod.mavg_i16(x, 32, 1).tobytes()).hexdigest() == digests["i16_n1048576_C1_k32"]
