@@ -27,6 +27,7 @@ __all__ = [
     "fill_synthetic",
     "workspace_bytes",
     "resolve_algo",
+    "plan",
     "ALGOS",
     "MavgError",
     "MavgLibraryError",
@@ -73,6 +74,14 @@ def workspace_bytes(n: int, grade: int, channels: int = 1, dtype: int = F32, alg
 
 def resolve_algo(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto") -> str:
     return algo_name(_lib.load().mavg_resolve_algo(n, channels, grade, dtype, _algo_code(algo)))
+
+
+def plan(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto") -> str:
+    """The kernel and launch geometry mavg_run would use (nothing is launched)."""
+    import ctypes
+    buf = ctypes.create_string_buffer(256)
+    _lib.check(_lib.load().mavg_plan(n, channels, grade, dtype, _algo_code(algo), buf, len(buf)), "mavg_plan")
+    return buf.value.decode()
 
 
 def moving_average_into(x, out, grade: int, channels: int = 1, algo="auto", history=None,

@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "mavg_workspace_bytes",
     "mavg_run",
     "mavg_resolve_algo",
+    "mavg_plan",
     "mavg_fill_synthetic",
     "mavg_strerror",
     "mavg_algo_name",
@@ -91,6 +92,8 @@ def load() -> ctypes.CDLL:
     lib.mavg_run.restype = i
     lib.mavg_resolve_algo.argtypes = [sz, i, i, i, i]
     lib.mavg_resolve_algo.restype = i
+    lib.mavg_plan.argtypes = [sz, i, i, i, i, ctypes.c_char_p, sz]
+    lib.mavg_plan.restype = i
     lib.mavg_fill_synthetic.argtypes = [vp, sz, i, u64, u64, i, vp]
     lib.mavg_fill_synthetic.restype = i
     lib.mavg_strerror.argtypes = [i]

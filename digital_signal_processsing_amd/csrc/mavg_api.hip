@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 
 #include "mavg_launch.hpp"
@@ -143,6 +144,21 @@ int mavg_run(const void* d_in, void* d_out, size_t n_samples, int channels, int 
     }
     default: return MAVG_ERR_INVALID_ARG;
   }
+}
+
+int mavg_plan(size_t n_samples, int channels, int grade, int dtype, int algo, char* buf, size_t buflen) {
+  if (buf == nullptr || buflen == 0) return MAVG_ERR_INVALID_ARG;
+  buf[0] = 0;
+  if (n_samples == 0) return MAVG_ERR_INVALID_ARG;
+  LaunchPlan plan{};
+  g_plan = &plan;
+  // aligned dummy device pointers: nothing is launched or dereferenced in plan mode
+  const int st = mavg_run(reinterpret_cast<const void*>(uintptr_t(1) << 20), reinterpret_cast<void*>(uintptr_t(1) << 21),
+                          n_samples, channels, grade, dtype, algo, 0, nullptr, nullptr, 0, nullptr);
+  g_plan = nullptr;
+  if (st != MAVG_OK) return st;
+  snprintf(buf, buflen, "%s", plan.text);
+  return MAVG_OK;
 }
 
 int mavg_fill_synthetic(void* d_out, size_t n_samples, int dtype, uint64_t seed, uint64_t offset, int dist,

@@ -4,6 +4,8 @@
 
 namespace mavg {
 
+thread_local LaunchPlan* g_plan = nullptr;
+
 // ---- per-device attribute cache (no stream work, capture-safe) --------------
 constexpr int kMaxDevices = 64;
 static std::atomic<int> g_cu_count[kMaxDevices];

@@ -147,9 +147,11 @@ struct Unit {
   T e[VE];
 };
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 template <int BYTES> struct RawVec;
-template <> struct RawVec<16> { using type = uint4; };
-template <> struct RawVec<8> { using type = uint2; };
+template <> struct RawVec<16> { using type = u32x4; };
+template <> struct RawVec<8> { using type = u32x2; };
 template <> struct RawVec<4> { using type = uint32_t; };
 template <> struct RawVec<2> { using type = uint16_t; };
 
@@ -158,12 +160,16 @@ struct UnitIO {
   static constexpr int kBytes = VE * (int)sizeof(T);
   static constexpr bool kVec = (kBytes == 16 || kBytes == 8 || kBytes == 4 || kBytes == 2);
 
-  // p is aligned to kBytes when kVec (checked on the host for the base pointer)
+  // p is aligned to kBytes when kVec (checked on the host for the base pointer).
+  // NT: non-temporal hint (streamed-once HBM data; never used on LDS).
+  template <bool NT = false>
   __device__ __forceinline__ static Unit<T, VE> load(const T* __restrict__ p) {
     Unit<T, VE> u;
     if constexpr (kVec) {
       using R = typename RawVec<kBytes>::type;
-      R r = *reinterpret_cast<const R*>(p);
+      R r;
+      if constexpr (NT) r = __builtin_nontemporal_load(reinterpret_cast<const R*>(p));
+      else r = *reinterpret_cast<const R*>(p);
       __builtin_memcpy(&u, &r, kBytes);
     } else {
 #pragma unroll
@@ -171,12 +177,14 @@ struct UnitIO {
     }
     return u;
   }
+  template <bool NT = false>
   __device__ __forceinline__ static void store(T* __restrict__ p, const Unit<T, VE>& u) {
     if constexpr (kVec) {
       using R = typename RawVec<kBytes>::type;
       R r;
       __builtin_memcpy(&r, &u, kBytes);
-      *reinterpret_cast<R*>(p) = r;
+      if constexpr (NT) __builtin_nontemporal_store(r, reinterpret_cast<R*>(p));
+      else *reinterpret_cast<R*>(p) = r;
     } else {
 #pragma unroll
       for (int i = 0; i < VE; ++i) p[i] = u.e[i];
@@ -254,10 +262,15 @@ struct ScanParams {
 };
 
 // T: sample type; A: accumulator; C: channels; F: frames per lane unit;
-// U: units per lane per chunk; HS: Hillis-Steele flavour.  p.xkg (uniform):
-// read x[n-k] from global memory instead of the LDS ring (very large k).
-template <typename T, typename A, int C, int F, int U, bool HS>
+// U: units per lane per chunk; HS: Hillis-Steele flavour; PD: chunks of
+// global loads kept in flight in registers (1 or 2); NT: bit 0 non-temporal
+// output stores, bit 1 non-temporal input loads.  p.xkg (uniform): read
+// x[n-k] from global memory instead of the LDS ring (very large k).
+constexpr int kNtStore = 1;
+constexpr int kNtLoad = 2;
+template <typename T, typename A, int C, int F, int U, bool HS, int PD = 1, int NT = 0>
 __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
+  static_assert(PD == 1 || PD == 2, "prefetch depth 1 or 2");
   constexpr int VE = F * C;                 // elements per unit
   constexpr int CHF = kWG * F * U;          // frames per chunk
   constexpr int NSEG = U * kNW;             // wave segments per chunk
@@ -293,7 +306,7 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long long f = c0 + (long long)(u * kWG + tid) * F;
-        buf[u] = IO::load(in + f * C);
+        buf[u] = IO::template load<(NT & kNtLoad) != 0>(in + f * C);
       }
     } else {
 #pragma unroll
@@ -312,16 +325,22 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
     for (int u = 0; u < U; ++u) IO::store(ring + (rpos + (u * kWG + tid) * F) * C, buf[u]);
   };
 
-  // ---- prologue: zero ring, stage chunk 0, prefetch chunk 1 ----------------
+  // ---- prologue: zero ring, stage chunk 0, prefetch chunks 1..PD -----------
   {
     uint4 z = make_uint4(0, 0, 0, 0);
     for (int i = tid * 16; i < ring_bytes; i += kWG * 16) *reinterpret_cast<uint4*>(smem + i) = z;
   }
-  U_t buf[U];
-  load_chunk(buf, p0);
+  // bufs[b] holds chunk ci+1 (b = (ci+1) % PD) at the top of iteration ci
+  U_t buf0[U], buf1[U];
+  load_chunk(buf0, p0);
   __syncthreads();
-  ring_write(buf, 0);
-  if (nch > 1) load_chunk(buf, p0 + CHF);
+  ring_write(buf0, 0);
+  if constexpr (PD == 1) {
+    if (nch > 1) load_chunk(buf0, p0 + CHF);
+  } else {
+    if (nch > 1) load_chunk(buf1, p0 + CHF);
+    if (nch > 2) load_chunk(buf0, p0 + 2LL * CHF);
+  }
   __syncthreads();
 
   A carry[C];
@@ -329,7 +348,8 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
   for (int c = 0; c < C; ++c) carry[c] = (A)0;
   int rpos = 0;
 
-  for (int ci = 0; ci < nch; ++ci) {
+  // one chunk: nb holds chunk ci+1 on entry and chunk ci+1+PD on exit
+  auto step = [&](const int ci, U_t (&nb)[U]) {
     const long long c0 = p0 + (long long)ci * CHF;
     const int par = ci & 1;
     // ring position (frames) of x[c0 - k]
@@ -408,8 +428,8 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
               if (fr >= s) {
                 t[fr][c] = v[u][fr - s][c];
               } else {
-                const A nb = shfl_up(v[u][fr - s + F][c], 1);
-                t[fr][c] = lane >= 1 ? nb : (A)0;
+                const A nbv = shfl_up(v[u][fr - s + F][c], 1);
+                t[fr][c] = lane >= 1 ? nbv : (A)0;
               }
             }
 #pragma unroll
@@ -423,8 +443,8 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
           for (int fr = 0; fr < F; ++fr)
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-              const A nb = shfl_up(v[u][fr][c], m);
-              v[u][fr][c] += lane >= m ? nb : (A)0;
+              const A nbv = shfl_up(v[u][fr][c], m);
+              v[u][fr][c] += lane >= m ? nbv : (A)0;
             }
         }
 #pragma unroll
@@ -436,12 +456,12 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
       }
     }
 
-    // (b) stage chunk ci+1 into the ring, prefetch chunk ci+2
+    // (b) stage chunk ci+1 into the ring, prefetch chunk ci+1+PD
     int rnext = rpos + CHF;
     if (rnext == R) rnext = 0;
     if (ci + 1 < nch) {
-      ring_write(buf, rnext);   // xkg: a 2-chunk ring holding x only
-      if (ci + 2 < nch) load_chunk(buf, c0 + 2LL * CHF);
+      ring_write(nb, rnext);   // xkg: a 2-chunk ring holding x only
+      if (ci + 1 + PD < nch) load_chunk(nb, c0 + (long long)(1 + PD) * CHF);
     }
 
     // (c) one barrier per chunk
@@ -483,7 +503,7 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
           for (int c = 0; c < C; ++c)
             y.e[fr * C + c] = to_out<T, A>(base[u][c] + lx[u][c] + v[u][fr][c], p.o);
         if (full) {
-          IO::store(out + f * C, y);
+          IO::template store<(NT & kNtStore) != 0>(out + f * C, y);
         } else {
 #pragma unroll
           for (int fr = 0; fr < F; ++fr)
@@ -494,6 +514,291 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
       }
     }
     rpos = rnext;
+  };
+
+  if constexpr (PD == 1) {
+    for (int ci = 0; ci < nch; ++ci) step(ci, buf0);
+  } else {
+    for (int ci = 0; ci < nch; ci += 2) {
+      step(ci, buf1);
+      if (ci + 1 < nch) step(ci + 1, buf0);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// flat-tile scan kernel: one short-lived workgroup per tile of T = 256*F*U
+// frames.  The carry into the tile is rebuilt from its k-frame halo instead
+// of being chained between workgroups:
+//     W[t0-1] = sum_{j=t0-k}^{t0-1} x[j]            (halo reduction)
+//     W[n]    = W[t0-1] + scan_{t0..n}(x[m] - x[m-k])
+// The halo and the tile are staged in LDS (x[n-k] reads); the tile's own
+// samples stay in registers.  Workgroups are remapped so that consecutive
+// tiles run on the same XCD: the halo is the tail of the tile that XCD just
+// read, an L2 hit, and all concurrently running workgroups of an XCD touch
+// one contiguous window of HBM (row-buffer locality: the "flat" access
+// shape that reaches 82% of HBM peak for a copy, tools/tune/membw.hip).
+// Two barriers per workgroup; no inter-workgroup communication.
+// ----------------------------------------------------------------------------
+struct TileParams {
+  const void* in;
+  void* out;
+  const void* hist;
+  long long nframes;
+  long long ntiles;
+  int k;
+  int halo_units;  // ceil(k / F): units staged before the tile
+  int xk_off;      // (-k*C) mod VE
+  int xcd_remap;   // 1: consecutive tiles on one XCD
+  OutParams o;
+};
+
+// GX: read x[n-k] and the halo straight from global memory (L1/L2 hits: the
+// tile was just loaded by this workgroup, the halo by the previous tile's
+// workgroup on the same XCD) instead of staging them in LDS; LDS then holds
+// only the scan totals, so the tile size no longer depends on k.
+template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, bool GX = false>
+__global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
+  constexpr int VE = F * C;
+  constexpr int TF = kWG * F * U;           // tile frames
+  constexpr int NSEG = U * kNW;
+  using IO = UnitIO<T, VE>;
+  using U_t = Unit<T, VE>;
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int Hu = p.halo_units;
+  const int Ha = Hu * F;                     // staged halo frames (>= k)
+  const int stage_bytes = GX ? 0 : ((((Hu + U * kWG + 1) * VE * (int)sizeof(T)) + 15) & ~15);
+  T* stage = reinterpret_cast<T*>(smem);     // [Hu + U*256 + 1 pad] units (LDS-staged variant)
+  A* tot = reinterpret_cast<A*>(smem + stage_bytes);  // [NSEG][C] segment totals
+  A* hsum = tot + NSEG * C;                            // [kNW][C] halo partial sums
+
+  const T* __restrict__ in = static_cast<const T*>(p.in);
+  T* __restrict__ out = static_cast<T*>(p.out);
+  const T* __restrict__ hist = static_cast<const T*>(p.hist);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int k = p.k;
+  const long long nframes = p.nframes;
+
+  // bijective XCD-aware remap (cdna_hip_programming.md 5.5 T1): blocks b and
+  // b+8 share an XCD; give each XCD a contiguous run of tiles.
+  long long tile = blockIdx.x;
+  if (p.xcd_remap) {
+    const long long nb = gridDim.x, b = blockIdx.x;
+    const long long q = nb / 8, r = nb % 8, x = b % 8;
+    tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+  }
+  const long long t0 = tile * TF;
+  const long long h0 = t0 - Ha;              // first staged halo frame
+  const bool tile_full = (t0 + TF <= nframes);
+
+  // ---- tile -> registers (streamed once: non-temporal) and LDS ----
+  U_t x[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long f = t0 + (long long)(u * kWG + tid) * F;
+    if (tile_full) {
+      x[u] = IO::template load<(NT & kNtLoad) != 0>(in + f * C);
+    } else {
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c) x[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+    }
+  }
+  if constexpr (!GX) {
+    // ---- halo -> LDS (re-read of the previous tile's tail: L2) ----
+    const bool halo_fast = h0 >= 0;
+    for (int j = tid; j < Hu; j += kWG) {
+      const long long f = h0 + (long long)j * F;
+      U_t h;
+      if (halo_fast) {
+        h = IO::load(in + f * C);
+      } else {
+#pragma unroll
+        for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+          for (int c = 0; c < C; ++c) h.e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+      }
+      IO::store(stage + j * VE, h);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) IO::store(stage + (Hu + u * kWG + tid) * VE, x[u]);
+    if (tid == 0) {
+      U_t z;
+#pragma unroll
+      for (int i = 0; i < VE; ++i) z.e[i] = (T)0;
+      IO::store(stage + (Hu + U * kWG) * VE, z);   // pad unit (k < F reads one unit past the tile)
+    }
+    __syncthreads();
+  }
+
+  // ---- halo reduction: W[t0-1] = sum of the k frames before t0 ----
+  {
+    A hs[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) hs[c] = (A)0;
+    if constexpr (!GX) {
+      for (int i = Ha - k + tid; i < Ha; i += kWG)
+#pragma unroll
+        for (int c = 0; c < C; ++c) hs[c] += to_acc<A>(stage[i * C + c]);
+    } else {
+      if (t0 - k >= 0) {
+        for (int i = tid; i < k; i += kWG)
+#pragma unroll
+          for (int c = 0; c < C; ++c) hs[c] += to_acc<A>(in[(t0 - k + i) * C + c]);
+      } else {
+        for (int i = tid; i < k; i += kWG)
+#pragma unroll
+          for (int c = 0; c < C; ++c) hs[c] += to_acc<A>(load_elem(in, hist, t0 - k + i, c, C, nframes, k));
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const A r = readlane(wave_incl_scan(hs[c]), 63);
+      if (lane == 0) hsum[w * C + c] = r;
+    }
+  }
+
+  // ---- d = x - x[n-k]; in-lane, wave and segment scans ----
+  A v[U][F][C];
+  A lx[U][C];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int j = u * kWG + tid;
+    const int e = (Ha + j * F - k) * C;      // LDS element of x[n-k]
+    U_t xk;
+    if constexpr (GX) {
+      const long long fk = t0 + (long long)j * F - k;    // first frame of x[n-k]
+      if (fk >= 0 && tile_full) {   // full tile: the straddle read stays below t0 + TF - k + VE
+        if constexpr (IO::kVec) {
+          if (p.xk_off == 0) {
+            xk = IO::load(in + fk * C);
+          } else {
+            const long long e_lo = fk * C - p.xk_off;
+            U_t a = IO::load(in + e_lo);
+            U_t b = IO::load(in + e_lo + VE);
+            xk = extract(a, b, p.xk_off);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < VE; ++i) xk.e[i] = in[fk * C + i];
+        }
+      } else {
+#pragma unroll
+        for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+          for (int c = 0; c < C; ++c) xk.e[fr * C + c] = load_elem(in, hist, fk + fr, c, C, nframes, k);
+      }
+    } else if constexpr (IO::kVec) {
+      if (p.xk_off == 0) {
+        xk = IO::load(stage + e);
+      } else {
+        const int e_lo = e - p.xk_off;
+        U_t a = IO::load(stage + e_lo);
+        U_t b = IO::load(stage + e_lo + VE);
+        xk = extract(a, b, p.xk_off);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < VE; ++i) xk.e[i] = stage[e + i];
+    }
+#pragma unroll
+    for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        v[u][fr][c] = to_acc<A>(x[u].e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
+    if constexpr (!HS) {
+#pragma unroll
+      for (int fr = 1; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c) v[u][fr][c] += v[u][fr - 1][c];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const A t = v[u][F - 1][c];
+        const A incl = wave_incl_scan(t);
+        lx[u][c] = incl - t;
+        const A segtot = readlane(incl, 63);
+        if (lane == 0) tot[(u * kNW + w) * C + c] = segtot;
+      }
+    } else {
+#pragma unroll
+      for (int s = 1; s < F; s <<= 1) {
+        A t[F][C];
+#pragma unroll
+        for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            if (fr >= s) {
+              t[fr][c] = v[u][fr - s][c];
+            } else {
+              const A nbv = shfl_up(v[u][fr - s + F][c], 1);
+              t[fr][c] = lane >= 1 ? nbv : (A)0;
+            }
+          }
+#pragma unroll
+        for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+          for (int c = 0; c < C; ++c) v[u][fr][c] += t[fr][c];
+      }
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) {
+#pragma unroll
+        for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            const A nbv = shfl_up(v[u][fr][c], m);
+            v[u][fr][c] += lane >= m ? nbv : (A)0;
+          }
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        lx[u][c] = (A)0;
+        const A segtot = readlane(v[u][F - 1][c], 63);
+        if (lane == 0) tot[(u * kNW + w) * C + c] = segtot;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- carry: halo sum + earlier segments; outputs ----
+  A base[U][C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    A w0 = (A)0;
+#pragma unroll
+    for (int i = 0; i < kNW; ++i) w0 += hsum[i * C + c];
+#pragma unroll
+    for (int u = 0; u < U; ++u) base[u][c] = w0;
+  }
+#pragma unroll
+  for (int s = 0; s < NSEG; ++s)
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const A t = tot[s * C + c];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (s < u * kNW + w) base[u][c] += t;
+    }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long f = t0 + (long long)(u * kWG + tid) * F;
+    U_t y;
+#pragma unroll
+    for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+      for (int c = 0; c < C; ++c) y.e[fr * C + c] = to_out<T, A>(base[u][c] + lx[u][c] + v[u][fr][c], p.o);
+    if (tile_full) {
+      IO::template store<(NT & kNtStore) != 0>(out + f * C, y);
+    } else {
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr)
+        if (f + fr < nframes)
+#pragma unroll
+          for (int c = 0; c < C; ++c) out[(f + fr) * C + c] = y.e[fr * C + c];
+    }
   }
 }
 

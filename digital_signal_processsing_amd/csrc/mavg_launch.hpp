@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <cstdio>
 
 #include "../../include/mavg.h"
 #include "mavg_kernels.hpp"
@@ -17,6 +18,20 @@ constexpr size_t kLdsBudget = 64 * 1024;  // per workgroup; keeps >= 2 workgroup
 
 int device_cu_count();
 OutParams make_out_params(int k);
+
+// Dry-run support for mavg_plan(): when g_plan is set (thread-local), the
+// launchers describe the launch they would make instead of making it.
+struct LaunchPlan {
+  char text[160];
+};
+extern thread_local LaunchPlan* g_plan;
+
+template <typename T> constexpr const char* type_name();
+template <> constexpr const char* type_name<float>() { return "f32"; }
+template <> constexpr const char* type_name<int16_t>() { return "i16"; }
+template <> constexpr const char* type_name<double>() { return "f64"; }
+template <> constexpr const char* type_name<int32_t>() { return "i32"; }
+template <> constexpr const char* type_name<int64_t>() { return "i64"; }
 
 // family entry points (defined in mavg_scan_*.hip / mavg_direct.hip)
 int scan_f32(int C, bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes, int k,
@@ -31,8 +46,15 @@ int naive_any(int dtype, bool wide, const void* in, void* out, const void* hist,
               hipStream_t st);
 
 // ---- streaming scan launch ----------------------------------------------------
-template <typename T, typename A, int C, int F, int U, bool HS>
-int launch_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st) {
+// Launch geometry knobs (tuned on MI355X with tools/tune).
+struct ScanTuning {
+  int oversub = 1;          // workgroups per resident slot (1 = one pass of long segments)
+  int min_seg_chunks = 1;   // lower bound on chunks per segment
+};
+
+template <typename T, typename A, int C, int F, int U, bool HS, int PD = 1, int NT = 0>
+int launch_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
+                ScanTuning tune = ScanTuning()) {
   constexpr int CHF = kWG * F * U;
   constexpr int NSEG = U * kNW;
   constexpr int VE = F * C;
@@ -60,30 +82,93 @@ int launch_scan(const void* in, void* out, const void* hist, long long nframes, 
 
   // one segment per workgroup; aim for every CU to hold a few workgroups
   const int wg_per_cu = std::max(1, std::min(8, (int)(160 * 1024 / lds)));
-  const long long target = (long long)device_cu_count() * wg_per_cu;
+  const long long target = (long long)device_cu_count() * wg_per_cu * std::max(1, tune.oversub);
   long long seg = (nframes + target - 1) / target;
-  seg = std::max<long long>(CHF, (seg + CHF - 1) / CHF * CHF);
+  seg = std::max<long long>((long long)CHF * std::max(1, tune.min_seg_chunks), (seg + CHF - 1) / CHF * CHF);
   p.seg_frames = seg;
   const long long nseg = (nframes + seg - 1) / seg;
   if (nseg > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
 
-  hipLaunchKernelGGL((scan_kernel<T, A, C, F, U, HS>), dim3((unsigned)nseg), dim3(kWG), lds, st, p);
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text),
+             "segment_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,pd=%d,nt=%d,xkg=%d> grid=%lld block=%d lds=%zu",
+             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", PD, NT, p.xkg, nseg, kWG, lds);
+    return MAVG_OK;
+  }
+  hipLaunchKernelGGL((scan_kernel<T, A, C, F, U, HS, PD, NT>), dim3((unsigned)nseg), dim3(kWG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
+// flat-tile scan: one workgroup per tile, carry rebuilt from the k-frame halo
+template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, bool GX = false>
+int launch_tile_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
+                     int xcd_remap = 1) {
+  constexpr int TF = kWG * F * U;
+  constexpr int NSEG = U * kNW;
+  constexpr int VE = F * C;
+  TileParams p{};
+  p.in = in;
+  p.out = out;
+  p.hist = hist;
+  p.nframes = nframes;
+  p.k = k;
+  p.o = make_out_params(k);
+  p.halo_units = (k + F - 1) / F;
+  p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
+  p.xcd_remap = xcd_remap;
+  p.ntiles = (nframes + TF - 1) / TF;
+  const size_t stage = GX ? 0 : ((((size_t)(p.halo_units + U * kWG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15);
+  const size_t lds = stage + (size_t)(NSEG + kNW) * C * sizeof(A);
+  if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
+  if (p.ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text),
+             "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,gx=%d> grid=%lld block=%d lds=%zu tile_frames=%d",
+             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)GX, p.ntiles, kWG, lds,
+             TF);
+    return MAVG_OK;
+  }
+  hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, GX>), dim3((unsigned)p.ntiles), dim3(kWG), lds, st, p);
+  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+}
+
+// Algorithm selection for the scan family (measured on MI355X with
+// tools/tune/tune_scan.hip, see DESIGN.md "Tuning"):
+//   * flat-tile scan with an LDS-staged halo whenever the halo fits: tile of
+//     2 units per lane (8 KiB of samples) for k*C*elem <= 8 KiB, 8 units per
+//     lane (32 KiB) for larger windows;
+//   * segment-streaming scan (LDS ring, pre-roll) when the halo does not fit
+//     the 64 KiB LDS budget; x[n-k] from global memory when even the ring
+//     does not fit.
+template <typename T, typename A, int C, int F, bool HS>
+int dispatch_scan_f(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st) {
+  constexpr int VE = F * C;
+  constexpr int kUnitBytes = VE * (int)sizeof(T);
+  const long long halo_bytes = (long long)k * C * (long long)sizeof(T);
+  auto tile_lds = [&](int U) -> long long {
+    const long long hu = (k + F - 1) / F;
+    return (hu + (long long)U * kWG + 1) * kUnitBytes + (U * kNW + kNW) * C * (long long)sizeof(A);
+  };
+  if (halo_bytes <= 8 * 1024 && tile_lds(2) <= (long long)kLdsBudget)
+    return launch_tile_scan<T, A, C, F, 2, HS, 0>(in, out, hist, nframes, k, st);
+  if (tile_lds(8) <= (long long)kLdsBudget)
+    return launch_tile_scan<T, A, C, F, 8, HS, 0>(in, out, hist, nframes, k, st);
+  constexpr int SU = F >= 4 ? 2 : 8;
+  return launch_scan<T, A, C, F, SU, HS, 2, kNtLoad | kNtStore>(in, out, hist, nframes, k, st);
+}
+
 template <typename T, typename A, int C>
-int dispatch_scan_c(bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes,
-                    int k, hipStream_t st) {
+int dispatch_scan_c(bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes, int k,
+                    hipStream_t st) {
   constexpr int VF = (C * (int)sizeof(T) <= 16 && 16 % (C * (int)sizeof(T)) == 0) ? 16 / (C * (int)sizeof(T)) : 0;
   if constexpr (VF > 0) {
     if (vec) {
-      constexpr int U = VF >= 4 ? 2 : 4;
-      return hs ? launch_scan<T, A, C, VF, U, true>(in, out, hist, nframes, k, st)
-                : launch_scan<T, A, C, VF, U, false>(in, out, hist, nframes, k, st);
+      return hs ? dispatch_scan_f<T, A, C, VF, true>(in, out, hist, nframes, k, st)
+                : dispatch_scan_f<T, A, C, VF, false>(in, out, hist, nframes, k, st);
     }
   }
-  return hs ? launch_scan<T, A, C, 1, 8, true>(in, out, hist, nframes, k, st)
-            : launch_scan<T, A, C, 1, 8, false>(in, out, hist, nframes, k, st);
+  return hs ? dispatch_scan_f<T, A, C, 1, true>(in, out, hist, nframes, k, st)
+            : dispatch_scan_f<T, A, C, 1, false>(in, out, hist, nframes, k, st);
 }
 
 template <typename T, typename A>
@@ -118,6 +203,11 @@ int launch_direct(const void* in, void* out, const void* hist, long long nframes
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   const long long nblk = (nframes + p.tile_frames - 1) / p.tile_frames;
   if (nblk > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text), "direct<%s,acc=%s,C=%d,F=%d> grid=%lld block=%d lds=%zu",
+             type_name<T>(), type_name<A>(), C, F, nblk, kWG, lds);
+    return MAVG_OK;
+  }
   hipLaunchKernelGGL((direct_kernel<T, A, C, F>), dim3((unsigned)nblk), dim3(kWG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
@@ -159,6 +249,11 @@ int launch_naive(const void* in, void* out, const void* hist, long long nframes,
   const long long n = nframes * C;
   const long long nblk = (n + kWG - 1) / kWG;
   if (nblk > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text), "naive<%s,acc=%s> grid=%lld block=%d", type_name<T>(),
+             type_name<A>(), nblk, kWG);
+    return MAVG_OK;
+  }
   hipLaunchKernelGGL((naive_kernel<T, A>), dim3((unsigned)nblk), dim3(kWG), 0, st, static_cast<const T*>(in),
                      static_cast<T*>(out), static_cast<const T*>(hist), nframes, C, k, make_out_params(k));
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;

@@ -96,6 +96,11 @@ int mavg_run(const void* d_in, void* d_out, size_t n_samples, int channels,
              int grade, int dtype, int algo, int block_size,
              const void* d_history, void* d_ws, size_t ws_bytes, void* stream);
 
+/* Describe, without launching anything, the kernel and launch geometry
+ * mavg_run would use for these arguments (e.g. "tile_scan<f32,...> grid=..."). */
+int mavg_plan(size_t n_samples, int channels, int grade, int dtype, int algo,
+              char* buf, size_t buflen);
+
 /* The algorithm MAVG_ALGO_AUTO resolves to for these arguments. */
 int mavg_resolve_algo(size_t n_samples, int channels, int grade, int dtype, int algo);
 

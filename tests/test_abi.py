@@ -82,3 +82,18 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_lib.MavgLibraryError):
         _lib.load()
+
+
+def test_plan_describes_launch_without_gpu():
+    import digital_signal_processsing_amd as dsp
+    p = dsp.plan(1 << 30, 1024)
+    assert p.startswith("tile_scan<f32,acc=f64,C=1,F=4,U=2,blelloch") and "grid=524288" in p, p
+    assert "U=8" in dsp.plan(1 << 30, 4096)
+    assert dsp.plan(1 << 20, 70_000).startswith("segment_scan<") and "xkg=1" in dsp.plan(1 << 20, 70_000)
+    assert dsp.plan(1 << 20, 7, algo="direct").startswith("direct<f32")
+    assert dsp.plan(1 << 20, 7, algo="naive").startswith("naive<f32")
+    assert "hillis" in dsp.plan(1 << 20, 7, algo="hillis_scalar")
+    assert dsp.plan(1 << 20, 100_000, dtype=dsp.I16).startswith("segment_scan<i16,acc=i64")
+    assert dsp.plan(3 * 1000, 7, channels=3, dtype=dsp.I16).startswith("tile_scan<i16,acc=i32,C=3,F=1")
+    with pytest.raises(dsp.MavgError):
+        dsp.plan(10, 0)

@@ -1,0 +1,180 @@
+// tune_scan.hip -- interleaved A/B timing of scan_kernel variants against an
+// HBM copy ceiling on one MI355X (cdna_hip_programming.md 5.4 rule 24: all
+// variants in ONE process, interleaved rounds, median and min reported).
+// Every scan variant's output is compared bit-for-bit with the first one.
+//
+// build: make -C tools/tune      run: tools/tune/tune_scan [log2n] [k] [rounds]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../digital_signal_processsing_amd/csrc/mavg_launch.hpp"
+
+using namespace mavg;
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+// float4 streaming copy: the achievable-bandwidth reference for 4 B in + 4 B out
+template <int NT, int UNR>
+__global__ __launch_bounds__(256) void copy_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out,
+                                                   long long n4) {
+  const long long stride = (long long)gridDim.x * 256 * UNR;
+  for (long long i = (long long)blockIdx.x * 256 * UNR + threadIdx.x; i < n4; i += stride) {
+    u32x4 v[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const long long j = i + u * 256;
+      if (j < n4) v[u] = (NT & 2) ? __builtin_nontemporal_load(in + j) : in[j];
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const long long j = i + u * 256;
+      if (j < n4) {
+        if (NT & 1) __builtin_nontemporal_store(v[u], out + j);
+        else out[j] = v[u];
+      }
+    }
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void flat_copy(const u32x4* __restrict__ in, u32x4* __restrict__ out, long long n4) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n4) {
+    u32x4 v = (NT & 2) ? __builtin_nontemporal_load(in + i) : in[i];
+    if (NT & 1) __builtin_nontemporal_store(v, out + i);
+    else out[i] = v;
+  }
+}
+
+__global__ void count_diff(const uint32_t* a, const uint32_t* b, long long n, unsigned long long* cnt) {
+  unsigned long long c = 0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    c += a[i] != b[i];
+  if (c) atomicAdd(cnt, c);
+}
+
+struct Variant {
+  std::string name;
+  bool is_scan;
+  std::function<int(hipStream_t)> launch;
+  std::vector<float> ms;
+  unsigned long long mism = 0;
+};
+
+int main(int argc, char** argv) {
+  const int lg = argc > 1 ? atoi(argv[1]) : 30;
+  const int k = argc > 2 ? atoi(argv[2]) : 1024;
+  const int rounds = argc > 3 ? atoi(argv[3]) : 10;
+  const long long n = 1LL << lg;
+  float *x, *y, *yref;
+  CK(hipMalloc(&x, n * 4));
+  CK(hipMalloc(&y, n * 4));
+  CK(hipMalloc(&yref, n * 4));
+  unsigned long long* dcnt;
+  CK(hipMalloc(&dcnt, 8));
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipLaunchKernelGGL(synth_kernel<float>, dim3(4096), dim3(256), 0, st, x, n, (uint64_t)0x5EED, 0);
+  CK(hipStreamSynchronize(st));
+  int cus = device_cu_count();
+  printf("device CUs=%d n=2^%d k=%d rounds=%d\n", cus, lg, k, rounds);
+
+  std::vector<Variant> vs;
+  const long long n4 = n / 4;
+  auto add_copy = [&](const char* nm, auto kern, int grid) {
+    vs.push_back({nm, false, [=](hipStream_t s) {
+                    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const u32x4*)x, (u32x4*)y, n4);
+                    return 0;
+                  }});
+  };
+  add_copy("copy gs g16384 u2 ntLS", copy_kernel<3, 2>, 16384);
+  add_copy("copy flat u1 ntLS", flat_copy<3>, (int)(n4 / 256));
+
+#define SCAN(U, PD, NT, OV)                                                                                  \
+  vs.push_back({"scan U" #U " PD" #PD " NT" #NT " ov" #OV, true, [=](hipStream_t s) {                       \
+                  ScanTuning t;                                                                             \
+                  t.oversub = OV;                                                                           \
+                  return launch_scan<float, double, 1, 4, U, false, PD, NT>(x, y, nullptr, n, k, s, t);     \
+                }});
+  SCAN(2, 2, 3, 1)
+  SCAN(1, 2, 1, 2)
+#define TILE(U, NT, RM)                                                                                  \
+  vs.push_back({"tile U" #U " NT" #NT " remap" #RM, true, [=](hipStream_t s) {                             \
+                  return launch_tile_scan<float, double, 1, 4, U, false, NT>(x, y, nullptr, n, k, s, RM);   \
+                }});
+#define TILEG(U, NT)                                                                                     \
+  vs.push_back({"tileG U" #U " NT" #NT, true, [=](hipStream_t s) {                                        \
+                  return launch_tile_scan<float, double, 1, 4, U, false, NT, true>(x, y, nullptr, n, k, s, 1); \
+                }});
+  TILE(1, 3, 1)
+  TILE(2, 3, 1)
+  TILE(2, 0, 1)
+  TILE(4, 0, 1)
+  TILE(8, 3, 1)
+  TILE(8, 0, 1)
+  TILEG(1, 3)
+  TILEG(2, 3)
+  TILEG(4, 3)
+  TILEG(8, 3)
+  TILEG(2, 0)
+  TILEG(4, 0)
+  TILEG(8, 0)
+  TILEG(4, 2)
+  TILEG(8, 2)
+
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  // reference output + correctness of every scan variant
+  bool have_ref = false;
+  for (auto& v : vs) {
+    if (!v.is_scan) continue;
+    if (v.launch(st) != 0) { printf("%s: launch failed\n", v.name.c_str()); return 1; }
+    CK(hipStreamSynchronize(st));
+    if (!have_ref) {
+      CK(hipMemcpyAsync(yref, y, n * 4, hipMemcpyDeviceToDevice, st));
+      have_ref = true;
+    } else {
+      CK(hipMemsetAsync(dcnt, 0, 8, st));
+      hipLaunchKernelGGL(count_diff, dim3(2048), dim3(256), 0, st, (const uint32_t*)y, (const uint32_t*)yref, n, dcnt);
+      CK(hipMemcpyAsync(&v.mism, dcnt, 8, hipMemcpyDeviceToHost, st));
+    }
+    CK(hipStreamSynchronize(st));
+    CK(hipMemsetAsync(y, 0xff, n * 4, st));
+  }
+  for (auto& v : vs) { v.launch(st); v.launch(st); }
+  CK(hipStreamSynchronize(st));
+  for (int r = 0; r < rounds; ++r) {
+    for (auto& v : vs) {
+      CK(hipEventRecord(e0, st));
+      v.launch(st);
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.ms.push_back(ms);
+    }
+  }
+  printf("%-28s %9s %9s %9s %9s %s\n", "variant", "med_ms", "min_ms", "GB/s", "frac8T", "mismatch");
+  for (auto& v : vs) {
+    std::vector<float> m = v.ms;
+    std::sort(m.begin(), m.end());
+    const float med = m[m.size() / 2], mn = m[0];
+    const double gbs = 8.0 * n / (med * 1e-3) / 1e9;
+    printf("%-28s %9.4f %9.4f %9.1f %9.4f %llu\n", v.name.c_str(), med, mn, gbs, gbs / 8000.0, v.mism);
+  }
+  return 0;
+}
