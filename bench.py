@@ -141,6 +141,7 @@ def run_workload(args, name, rank, world, with_cpu):
     y = torch.empty_like(x)
     hist_buf = torch.empty(max((k - 1) * C, 1), dtype=dtype, device="cuda")
     resolved = dsp.resolve_algo(n, k, C, dsp.F32 if dt == "f32" else dsp.I16, algo)
+    launch_plan = dsp.plan(n, k, C, dsp.F32 if dt == "f32" else dsp.I16, algo)
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
@@ -202,7 +203,7 @@ def run_workload(args, name, rank, world, with_cpu):
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": f"scan_kernel/{resolved}" if "direct" not in resolved else f"direct_kernel/{resolved}",
+            "kernel": launch_plan,
             "kernel_avg_ms": round(kern_avg_ms, 4),
             "kernel_min_ms": round(min(kern_ms), 4),
             "algorithmic_bytes_per_launch": alg_bytes,

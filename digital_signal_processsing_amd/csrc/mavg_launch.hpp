@@ -188,8 +188,11 @@ int dispatch_scan(int C, bool vec, bool hs, const void* in, void* out, const voi
 }
 
 // ---- direct LDS-tiled launch ---------------------------------------------------
-template <typename T, typename A, int C, int F>
-int launch_direct(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st) {
+template <typename T, typename A, int C, int F, int U = 2>
+int launch_direct(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
+                  int xcd_remap = 1) {
+  constexpr int TF = kWG * F * U;
+  constexpr int VE = F * C;
   DirectParams p{};
   p.in = in;
   p.out = out;
@@ -197,18 +200,19 @@ int launch_direct(const void* in, void* out, const void* hist, long long nframes
   p.nframes = nframes;
   p.k = k;
   p.o = make_out_params(k);
-  p.halo_frames = ((k - 1) + F - 1) / F * F;
-  p.tile_frames = kWG * F * 4;
-  const size_t lds = (((size_t)(p.halo_frames + p.tile_frames) * C * sizeof(T)) + 15) & ~(size_t)15;
+  p.m = (k - 1 + F - 1) / F;
+  p.off = p.m * F - (k - 1);
+  p.xcd_remap = xcd_remap;
+  const size_t lds = (((size_t)(p.m + U * kWG) * VE * sizeof(T)) + 15) & ~(size_t)15;
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
-  const long long nblk = (nframes + p.tile_frames - 1) / p.tile_frames;
+  const long long nblk = (nframes + TF - 1) / TF;
   if (nblk > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
-    snprintf(g_plan->text, sizeof(g_plan->text), "direct<%s,acc=%s,C=%d,F=%d> grid=%lld block=%d lds=%zu",
-             type_name<T>(), type_name<A>(), C, F, nblk, kWG, lds);
+    snprintf(g_plan->text, sizeof(g_plan->text), "direct<%s,acc=%s,C=%d,F=%d,U=%d> grid=%lld block=%d lds=%zu",
+             type_name<T>(), type_name<A>(), C, F, U, nblk, kWG, lds);
     return MAVG_OK;
   }
-  hipLaunchKernelGGL((direct_kernel<T, A, C, F>), dim3((unsigned)nblk), dim3(kWG), lds, st, p);
+  hipLaunchKernelGGL((direct_kernel<T, A, C, F, U>), dim3((unsigned)nblk), dim3(kWG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 

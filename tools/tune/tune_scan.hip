@@ -119,21 +119,19 @@ int main(int argc, char** argv) {
   vs.push_back({"tileG U" #U " NT" #NT, true, [=](hipStream_t s) {                                        \
                   return launch_tile_scan<float, double, 1, 4, U, false, NT, true>(x, y, nullptr, n, k, s, 1); \
                 }});
+#define DIRECT(U, RM)                                                                                   \
+  vs.push_back({"direct U" #U " remap" #RM, true, [=](hipStream_t s) {                                     \
+                  return launch_direct<float, double, 1, 4, U>(x, y, nullptr, n, k, s, RM);                \
+                }});
   TILE(1, 3, 1)
-  TILE(2, 3, 1)
   TILE(2, 0, 1)
   TILE(4, 0, 1)
-  TILE(8, 3, 1)
   TILE(8, 0, 1)
-  TILEG(1, 3)
-  TILEG(2, 3)
-  TILEG(4, 3)
-  TILEG(8, 3)
-  TILEG(2, 0)
-  TILEG(4, 0)
-  TILEG(8, 0)
-  TILEG(4, 2)
-  TILEG(8, 2)
+  TILE(2, 3, 1)
+  DIRECT(1, 1)
+  DIRECT(2, 1)
+  DIRECT(4, 1)
+  DIRECT(2, 0)
 
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
