@@ -188,7 +188,7 @@ int dispatch_scan(int C, bool vec, bool hs, const void* in, void* out, const voi
 }
 
 // ---- direct LDS-tiled launch ---------------------------------------------------
-template <typename T, typename A, int C, int F, int U = 2>
+template <typename T, typename A, int C, int F, int U = 1>
 int launch_direct(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
                   int xcd_remap = 1) {
   constexpr int TF = kWG * F * U;

@@ -94,6 +94,12 @@ def test_plan_describes_launch_without_gpu():
     assert dsp.plan(1 << 20, 7, algo="naive").startswith("naive<f32")
     assert "hillis" in dsp.plan(1 << 20, 7, algo="hillis_scalar")
     assert dsp.plan(1 << 20, 100_000, dtype=dsp.I16).startswith("segment_scan<i16,acc=i64")
-    assert dsp.plan(3 * 1000, 7, channels=3, dtype=dsp.I16).startswith("tile_scan<i16,acc=i32,C=3,F=1")
+    assert dsp.plan(3 * 1000, 7, channels=3, dtype=dsp.I16, algo="blelloch").startswith("tile_scan<i16,acc=i32,C=3,F=1")
     with pytest.raises(dsp.MavgError):
         dsp.plan(10, 0)
+
+
+def test_auto_picks_direct_for_tiny_windows():
+    import digital_signal_processsing_amd as dsp
+    assert dsp.resolve_algo(1 << 20, 7) == "direct" and dsp.resolve_algo(1 << 20, 9) == "direct"
+    assert dsp.resolve_algo(1 << 20, 10) == "blelloch" and dsp.resolve_algo(1 << 20, 1024) == "blelloch"
