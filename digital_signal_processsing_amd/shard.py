@@ -23,33 +23,49 @@ def shard_bounds(total_frames: int, world: int, rank: int) -> Tuple[int, int]:
     return f0, f1
 
 
-def exchange_halo(x_local, grade: int, channels: int = 1, group=None, recv_buf=None):
-    """Send this shard's last (grade-1)*channels samples to rank+1 and receive
-    rank-1's into the returned history tensor (None on rank 0 or when
-    grade == 1).  Works for any backend whose tensors live where `x_local`
-    lives.  Each shard must hold at least grade-1 frames.
-    """
+def head_frames(grade: int, nframes: int) -> int:
+    """Frames at the start of a shard whose window reaches into the previous
+    shard: [0, grade-1), rounded up to 64 frames so the interior launch starts
+    16-byte aligned."""
+    if grade <= 1:
+        return 0
+    return min(nframes, (grade - 1 + 63) // 64 * 64)
+
+
+def start_halo_exchange(x_local, grade: int, channels: int = 1, group=None, recv_buf=None):
+    """Post the halo send (this shard's last (grade-1)*channels samples to
+    rank+1) and receive (rank-1's tail); returns (requests, history) where
+    history is None on rank 0 / grade 1.  Wait on the requests before using
+    history; with NCCL (= RCCL) the wait makes the current stream wait."""
     import torch
     import torch.distributed as dist
 
+    if not (dist.is_available() and dist.is_initialized()):
+        return [], None
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     h = (grade - 1) * channels
     if h == 0 or world == 1:
-        return None
+        return [], None
     if x_local.numel() < h:
         raise ValueError(f"shard holds {x_local.numel()} samples < halo {h}: use fewer ranks or a smaller grade")
     ops = []
     if rank + 1 < world:
-        tail = x_local[x_local.numel() - h:].contiguous()
+        tail = x_local[x_local.numel() - h:]
         ops.append(dist.P2POp(dist.isend, tail, _peer(rank + 1, group), group))
     hist = None
     if rank > 0:
         hist = recv_buf if recv_buf is not None else torch.empty(h, dtype=x_local.dtype, device=x_local.device)
         ops.append(dist.P2POp(dist.irecv, hist, _peer(rank - 1, group), group))
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+    reqs = dist.batch_isend_irecv(ops) if ops else []
+    return reqs, hist
+
+
+def exchange_halo(x_local, grade: int, channels: int = 1, group=None, recv_buf=None):
+    """Blocking form of start_halo_exchange: returns the history tensor."""
+    reqs, hist = start_halo_exchange(x_local, grade, channels, group, recv_buf)
+    for r in reqs:
+        r.wait()
     return hist
 
 
@@ -60,15 +76,48 @@ def _peer(group_rank: int, group) -> int:
     return dist.get_global_rank(group, group_rank)
 
 
-def sharded_moving_average(x_local, grade: int, channels: int = 1, algo="auto", group=None,
-                           out=None, recv_buf=None):
-    """Moving average of the global signal whose shard this rank holds
-    (device tensor); returns this rank's shard of the output."""
+def split_moving_average_into(x_local, out, grade: int, channels: int = 1, algo="auto", history=None,
+                              events=None, before_head=None) -> None:
+    """out = moving average of x_local given `history` (the (grade-1)*channels
+    samples before it, None = zeros) as two launches: the interior (frames >=
+    head_frames(), history taken from inside x_local) first, then -- after
+    `before_head()` (e.g. waiting for the halo) -- the head.  Same result as
+    one launch with `history`; the split only lets the halo arrive late."""
     from . import moving_average_into
+
+    C = channels
+    nframes = x_local.numel() // C
+    head = head_frames(grade, nframes)
+    if head < nframes:
+        if events is not None:
+            events[0].record()
+        interior_hist = x_local[(head - (grade - 1)) * C: head * C] if head > 0 else None
+        moving_average_into(x_local[head * C:], out[head * C:], grade, C, algo, history=interior_hist)
+        if events is not None:
+            events[1].record()
+    if before_head is not None:
+        before_head()
+    if head > 0:
+        moving_average_into(x_local[: head * C], out[: head * C], grade, C, algo,
+                            history=history() if callable(history) else history)
+
+
+def sharded_moving_average(x_local, grade: int, channels: int = 1, algo="auto", group=None,
+                           out=None, recv_buf=None, events=None):
+    """Moving average of the global signal whose shard this rank holds
+    (device tensor); returns this rank's shard of the output.  The halo
+    send/recv is posted first and overlaps the interior launch; only the head
+    launch waits for it.  `events` = optional (start, end) CUDA events around
+    the interior launch (bench.py's roofline timing)."""
     import torch
 
-    hist = exchange_halo(x_local, grade, channels, group, recv_buf)
     if out is None:
         out = torch.empty_like(x_local)
-    moving_average_into(x_local, out, grade, channels, algo, history=hist)
+    reqs, hist = start_halo_exchange(x_local, grade, channels, group, recv_buf)
+
+    def wait():
+        for r in reqs:
+            r.wait()
+
+    split_moving_average_into(x_local, out, grade, channels, algo, history=hist, events=events, before_head=wait)
     return out

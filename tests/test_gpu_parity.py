@@ -189,3 +189,35 @@ def test_checksum_of_checksums_repeatability(gpu):
         d = torch.sum(y.view(torch.int32).to(torch.int64) * 2654435761 % (1 << 31)).item()
         assert h is None or d == h
         h = d
+
+
+@pytest.mark.parametrize("C,k,dtype", [(1, 1024, "f32"), (2, 41, "i16"), (1, 1, "f32"), (1, 4096, "f32"),
+                                       (2, 70, "f32")])
+def test_sharded_split_launch_equals_whole_signal(oracle_mod, gpu, C, k, dtype):
+    """The multi-GPU step on one GPU: every shard filtered as interior launch +
+    head launch with the previous shard's tail as history (what rank r does
+    after the RCCL halo arrives) reproduces the whole-signal output."""
+    import torch
+    from digital_signal_processsing_amd.shard import shard_bounds, split_moving_average_into
+    frames, world = 300_001, 4
+    if dtype == "i16":
+        x = oracle_mod.synth_i16(frames * C, offset=k)
+        full = oracle_mod.mavg_i16(x, k, C)
+    else:
+        x = oracle_mod.synth_f32(frames * C, offset=k, dist=1)
+        full = oracle_mod.mavg_f32(x, k, C)
+    xd = torch.from_numpy(x).to(gpu)
+    out = torch.empty_like(xd)
+    for r in range(world):
+        f0, f1 = shard_bounds(frames, world, r)
+        hist = xd[(f0 - (k - 1)) * C: f0 * C] if (r > 0 and k > 1) else None
+        # shards must start 16-B aligned for the vector kernels: copy each into its own buffer
+        xl = xd[f0 * C: f1 * C].clone()
+        ol = torch.empty_like(xl)
+        split_moving_average_into(xl, ol, k, C, "blelloch", history=hist.clone() if hist is not None else None)
+        out[f0 * C: f1 * C] = ol
+    y = out.cpu().numpy()
+    if dtype == "i16":
+        assert np.array_equal(y, full)
+    else:
+        assert_f32_close(y, full, f"C={C} k={k}")
