@@ -36,6 +36,11 @@ WORKLOADS = {
     "blelloch_2p26": (1 << 26, 64, 1, "f32", "blelloch"),   # configs[1]
     "direct_2p28": (1 << 28, 7, 1, "f32", "direct"),        # configs[2]
     "carry_2p30": (1 << 30, 4096, 1, "f32", "blelloch"),    # configs[3]
+    # secondary lines (--all-workloads): the reference's own int16 PCM data path,
+    # stereo as in its WAV harness, and the Hillis-Steele flavour of the scan
+    "i16_2p30": (1 << 30, 1024, 1, "i16", "blelloch"),
+    "i16_stereo_2p30": (1 << 30, 1024, 2, "i16", "blelloch"),
+    "hillis_2p30": (1 << 30, 1024, 1, "f32", "hillis"),
 }
 
 

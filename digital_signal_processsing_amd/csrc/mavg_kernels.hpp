@@ -258,8 +258,31 @@ struct ScanParams {
   int pre_chunks;        // pre-roll chunks per segment (ceil((k-1)/chunk))
   int xk_off;            // (-k*C) mod VE, elements: offset of x[n-k] inside its aligned unit
   int xkg;               // 1: read x[n-k] from global memory (k too large for the LDS ring)
+  int xcd_remap;         // remap mode (remap_tile): 0 identity, 1 contiguous per XCD, G>1 grouped
   OutParams o;
 };
+
+// bijective remap: blocks b and b+8 share an XCD (observed round-robin
+// dispatch, cdna_hip_programming.md 5.5 T1); give each XCD a contiguous run.
+__device__ __forceinline__ long long xcd_contiguous(long long b, long long nb) {
+  const long long q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+// grouped remap: every XCD takes runs of G consecutive tiles and the eight
+// XCDs' runs are adjacent, so the whole chip works inside one window of 8*G
+// tiles (tail blocks beyond the last full group map to themselves).
+__device__ __forceinline__ long long xcd_grouped(long long b, long long nb, long long G) {
+  const long long full = nb / (8 * G) * (8 * G);
+  if (b >= full) return b;
+  const long long i = b / 8, x = b % 8;
+  return (i / G) * (8 * G) + x * G + (i % G);
+}
+// remap mode: 0 identity, 1 contiguous run per XCD, G > 1: grouped with G tiles
+__device__ __forceinline__ long long remap_tile(long long b, long long nb, int mode) {
+  if (mode == 0) return b;
+  if (mode == 1) return xcd_contiguous(b, nb);
+  return xcd_grouped(b, nb, mode);
+}
 
 // T: sample type; A: accumulator; C: channels; F: frames per lane unit;
 // U: units per lane per chunk; HS: Hillis-Steele flavour; PD: chunks of
@@ -295,7 +318,8 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
   const int k = p.k;
   const int R = p.ring_frames;
 
-  const long long s0 = (long long)blockIdx.x * p.seg_frames;
+  const long long seg = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
+  const long long s0 = seg * p.seg_frames;
   const long long s1 = min(s0 + p.seg_frames, nframes);
   const long long p0 = s0 - (long long)p.pre_chunks * CHF;
   const int nch = p.pre_chunks + (int)((s1 - s0 + CHF - 1) / CHF);
@@ -549,7 +573,7 @@ struct TileParams {
   int k;
   int halo_units;  // ceil(k / F): units staged before the tile
   int xk_off;      // (-k*C) mod VE
-  int xcd_remap;   // 1: consecutive tiles on one XCD
+  int xcd_remap;   // remap mode (remap_tile): 0 identity, 1 contiguous per XCD, G>1 grouped
   OutParams o;
 };
 
@@ -557,21 +581,23 @@ struct TileParams {
 // tile was just loaded by this workgroup, the halo by the previous tile's
 // workgroup on the same XCD) instead of staging them in LDS; LDS then holds
 // only the scan totals, so the tile size no longer depends on k.
-template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, bool GX = false>
-__global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
+template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, bool GX = false,
+          int WG = kWG>
+__global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
+  constexpr int NW = WG / 64;
   constexpr int VE = F * C;
-  constexpr int TF = kWG * F * U;           // tile frames
-  constexpr int NSEG = U * kNW;
+  constexpr int TF = WG * F * U;           // tile frames
+  constexpr int NSEG = U * NW;
   using IO = UnitIO<T, VE>;
   using U_t = Unit<T, VE>;
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int Hu = p.halo_units;
   const int Ha = Hu * F;                     // staged halo frames (>= k)
-  const int stage_bytes = GX ? 0 : ((((Hu + U * kWG + 1) * VE * (int)sizeof(T)) + 15) & ~15);
+  const int stage_bytes = GX ? 0 : ((((Hu + U * WG + 1) * VE * (int)sizeof(T)) + 15) & ~15);
   T* stage = reinterpret_cast<T*>(smem);     // [Hu + U*256 + 1 pad] units (LDS-staged variant)
   A* tot = reinterpret_cast<A*>(smem + stage_bytes);  // [NSEG][C] segment totals
-  A* hsum = tot + NSEG * C;                            // [kNW][C] halo partial sums
+  A* hsum = tot + NSEG * C;                            // [NW][C] halo partial sums
 
   const T* __restrict__ in = static_cast<const T*>(p.in);
   T* __restrict__ out = static_cast<T*>(p.out);
@@ -584,12 +610,7 @@ __global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
 
   // bijective XCD-aware remap (cdna_hip_programming.md 5.5 T1): blocks b and
   // b+8 share an XCD; give each XCD a contiguous run of tiles.
-  long long tile = blockIdx.x;
-  if (p.xcd_remap) {
-    const long long nb = gridDim.x, b = blockIdx.x;
-    const long long q = nb / 8, r = nb % 8, x = b % 8;
-    tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-  }
+  const long long tile = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
   const long long t0 = tile * TF;
   const long long h0 = t0 - Ha;              // first staged halo frame
   const bool tile_full = (t0 + TF <= nframes);
@@ -598,7 +619,7 @@ __global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
   U_t x[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const long long f = t0 + (long long)(u * kWG + tid) * F;
+    const long long f = t0 + (long long)(u * WG + tid) * F;
     if (tile_full) {
       x[u] = IO::template load<(NT & kNtLoad) != 0>(in + f * C);
     } else {
@@ -611,7 +632,7 @@ __global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
   if constexpr (!GX) {
     // ---- halo -> LDS (re-read of the previous tile's tail: L2) ----
     const bool halo_fast = h0 >= 0;
-    for (int j = tid; j < Hu; j += kWG) {
+    for (int j = tid; j < Hu; j += WG) {
       const long long f = h0 + (long long)j * F;
       U_t h;
       if (halo_fast) {
@@ -625,12 +646,12 @@ __global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
       IO::store(stage + j * VE, h);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) IO::store(stage + (Hu + u * kWG + tid) * VE, x[u]);
+    for (int u = 0; u < U; ++u) IO::store(stage + (Hu + u * WG + tid) * VE, x[u]);
     if (tid == 0) {
       U_t z;
 #pragma unroll
       for (int i = 0; i < VE; ++i) z.e[i] = (T)0;
-      IO::store(stage + (Hu + U * kWG) * VE, z);   // pad unit (k < F reads one unit past the tile)
+      IO::store(stage + (Hu + U * WG) * VE, z);   // pad unit (k < F reads one unit past the tile)
     }
     __syncthreads();
   }
@@ -641,16 +662,16 @@ __global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
 #pragma unroll
     for (int c = 0; c < C; ++c) hs[c] = (A)0;
     if constexpr (!GX) {
-      for (int i = Ha - k + tid; i < Ha; i += kWG)
+      for (int i = Ha - k + tid; i < Ha; i += WG)
 #pragma unroll
         for (int c = 0; c < C; ++c) hs[c] += to_acc<A>(stage[i * C + c]);
     } else {
       if (t0 - k >= 0) {
-        for (int i = tid; i < k; i += kWG)
+        for (int i = tid; i < k; i += WG)
 #pragma unroll
           for (int c = 0; c < C; ++c) hs[c] += to_acc<A>(in[(t0 - k + i) * C + c]);
       } else {
-        for (int i = tid; i < k; i += kWG)
+        for (int i = tid; i < k; i += WG)
 #pragma unroll
           for (int c = 0; c < C; ++c) hs[c] += to_acc<A>(load_elem(in, hist, t0 - k + i, c, C, nframes, k));
       }
@@ -667,7 +688,7 @@ __global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
   A lx[U][C];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int j = u * kWG + tid;
+    const int j = u * WG + tid;
     const int e = (Ha + j * F - k) * C;      // LDS element of x[n-k]
     U_t xk;
     if constexpr (GX) {
@@ -721,7 +742,7 @@ __global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
         const A incl = wave_incl_scan(t);
         lx[u][c] = incl - t;
         const A segtot = readlane(incl, 63);
-        if (lane == 0) tot[(u * kNW + w) * C + c] = segtot;
+        if (lane == 0) tot[(u * NW + w) * C + c] = segtot;
       }
     } else {
 #pragma unroll
@@ -757,7 +778,7 @@ __global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
       for (int c = 0; c < C; ++c) {
         lx[u][c] = (A)0;
         const A segtot = readlane(v[u][F - 1][c], 63);
-        if (lane == 0) tot[(u * kNW + w) * C + c] = segtot;
+        if (lane == 0) tot[(u * NW + w) * C + c] = segtot;
       }
     }
   }
@@ -769,7 +790,7 @@ __global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
   for (int c = 0; c < C; ++c) {
     A w0 = (A)0;
 #pragma unroll
-    for (int i = 0; i < kNW; ++i) w0 += hsum[i * C + c];
+    for (int i = 0; i < NW; ++i) w0 += hsum[i * C + c];
 #pragma unroll
     for (int u = 0; u < U; ++u) base[u][c] = w0;
   }
@@ -780,11 +801,11 @@ __global__ __launch_bounds__(kWG) void tile_scan_kernel(TileParams p) {
       const A t = tot[s * C + c];
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (s < u * kNW + w) base[u][c] += t;
+        if (s < u * NW + w) base[u][c] += t;
     }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const long long f = t0 + (long long)(u * kWG + tid) * F;
+    const long long f = t0 + (long long)(u * WG + tid) * F;
     U_t y;
 #pragma unroll
     for (int fr = 0; fr < F; ++fr)
@@ -858,10 +879,10 @@ __device__ __forceinline__ void pick_prefix_rt(int off, const A (&pc)[2 * F][C],
   }
 }
 
-template <typename T, typename A, int C, int F, int U>
-__global__ __launch_bounds__(kWG) void direct_kernel(DirectParams p) {
+template <typename T, typename A, int C, int F, int U, int WG = kWG>
+__global__ __launch_bounds__(WG) void direct_kernel(DirectParams p) {
   constexpr int VE = F * C;
-  constexpr int TF = kWG * F * U;
+  constexpr int TF = WG * F * U;
   using IO = UnitIO<T, VE>;
   using U_t = Unit<T, VE>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -875,12 +896,7 @@ __global__ __launch_bounds__(kWG) void direct_kernel(DirectParams p) {
   const int m = p.m;
   const long long nframes = p.nframes;
 
-  long long tile = blockIdx.x;
-  if (p.xcd_remap) {
-    const long long nb = gridDim.x, b = blockIdx.x;
-    const long long q = nb / 8, r = nb % 8, x = b % 8;
-    tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-  }
+  const long long tile = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
   const long long t0 = tile * TF;
   const long long h0 = t0 - (long long)m * F;
   const bool tile_full = (t0 + TF <= nframes);
@@ -888,7 +904,7 @@ __global__ __launch_bounds__(kWG) void direct_kernel(DirectParams p) {
   U_t xr[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const long long f = t0 + (long long)(u * kWG + tid) * F;
+    const long long f = t0 + (long long)(u * WG + tid) * F;
     if (tile_full) {
       xr[u] = IO::load(in + f * C);
     } else {
@@ -899,7 +915,7 @@ __global__ __launch_bounds__(kWG) void direct_kernel(DirectParams p) {
     }
   }
   const bool halo_fast = h0 >= 0;
-  for (int j = tid; j < m; j += kWG) {
+  for (int j = tid; j < m; j += WG) {
     const long long f = h0 + (long long)j * F;
     U_t h;
     if (halo_fast) {
@@ -913,12 +929,12 @@ __global__ __launch_bounds__(kWG) void direct_kernel(DirectParams p) {
     IO::store(stage + j * VE, h);
   }
 #pragma unroll
-  for (int u = 0; u < U; ++u) IO::store(stage + (m + u * kWG + tid) * VE, xr[u]);
+  for (int u = 0; u < U; ++u) IO::store(stage + (m + u * WG + tid) * VE, xr[u]);
   __syncthreads();
 
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int q = m + u * kWG + tid;  // own unit in the stage
+    const int q = m + u * WG + tid;  // own unit in the stage
     A own[F][C];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
@@ -972,7 +988,7 @@ __global__ __launch_bounds__(kWG) void direct_kernel(DirectParams p) {
 #pragma unroll
         for (int c = 0; c < C; ++c) wsum[fr][c] = tot[c] + own[fr][c] - pre[fr][c];
     }
-    const long long f = t0 + (long long)(u * kWG + tid) * F;
+    const long long f = t0 + (long long)(u * WG + tid) * F;
     U_t y;
 #pragma unroll
     for (int fr = 0; fr < F; ++fr)

@@ -50,6 +50,8 @@ int naive_any(int dtype, bool wide, const void* in, void* out, const void* hist,
 struct ScanTuning {
   int oversub = 1;          // workgroups per resident slot (1 = one pass of long segments)
   int min_seg_chunks = 1;   // lower bound on chunks per segment
+  int seg_chunks = 0;       // > 0: fixed segment length in chunks (overrides the two above)
+  int xcd_remap = 0;        // 1: consecutive segments on one XCD
 };
 
 template <typename T, typename A, int C, int F, int U, bool HS, int PD = 1, int NT = 0>
@@ -85,7 +87,9 @@ int launch_scan(const void* in, void* out, const void* hist, long long nframes, 
   const long long target = (long long)device_cu_count() * wg_per_cu * std::max(1, tune.oversub);
   long long seg = (nframes + target - 1) / target;
   seg = std::max<long long>((long long)CHF * std::max(1, tune.min_seg_chunks), (seg + CHF - 1) / CHF * CHF);
+  if (tune.seg_chunks > 0) seg = (long long)CHF * tune.seg_chunks;
   p.seg_frames = seg;
+  p.xcd_remap = tune.xcd_remap;
   const long long nseg = (nframes + seg - 1) / seg;
   if (nseg > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
 
@@ -100,11 +104,12 @@ int launch_scan(const void* in, void* out, const void* hist, long long nframes, 
 }
 
 // flat-tile scan: one workgroup per tile, carry rebuilt from the k-frame halo
-template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, bool GX = false>
+template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, bool GX = false,
+          int WG = kWG>
 int launch_tile_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
                      int xcd_remap = 1) {
-  constexpr int TF = kWG * F * U;
-  constexpr int NSEG = U * kNW;
+  constexpr int TF = WG * F * U;
+  constexpr int NSEG = U * (WG / 64);
   constexpr int VE = F * C;
   TileParams p{};
   p.in = in;
@@ -117,18 +122,18 @@ int launch_tile_scan(const void* in, void* out, const void* hist, long long nfra
   p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
   p.xcd_remap = xcd_remap;
   p.ntiles = (nframes + TF - 1) / TF;
-  const size_t stage = GX ? 0 : ((((size_t)(p.halo_units + U * kWG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15);
-  const size_t lds = stage + (size_t)(NSEG + kNW) * C * sizeof(A);
+  const size_t stage = GX ? 0 : ((((size_t)(p.halo_units + U * WG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15);
+  const size_t lds = stage + (size_t)(NSEG + WG / 64) * C * sizeof(A);
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   if (p.ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
              "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,gx=%d> grid=%lld block=%d lds=%zu tile_frames=%d",
-             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)GX, p.ntiles, kWG, lds,
+             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)GX, p.ntiles, WG, lds,
              TF);
     return MAVG_OK;
   }
-  hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, GX>), dim3((unsigned)p.ntiles), dim3(kWG), lds, st, p);
+  hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, GX, WG>), dim3((unsigned)p.ntiles), dim3(WG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
@@ -153,8 +158,15 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
     return launch_tile_scan<T, A, C, F, 2, HS, 0>(in, out, hist, nframes, k, st);
   if (tile_lds(8) <= (long long)kLdsBudget)
     return launch_tile_scan<T, A, C, F, 8, HS, 0>(in, out, hist, nframes, k, st);
+  // segment streaming: short XCD-remapped segments of at least 4 chunks and
+  // 4x the pre-roll (measured 5.5-5.7 TB/s vs 5.0 for one long segment per
+  // workgroup, tools/tune/tune_scan.hip)
   constexpr int SU = F >= 4 ? 2 : 8;
-  return launch_scan<T, A, C, F, SU, HS, 2, kNtLoad | kNtStore>(in, out, hist, nframes, k, st);
+  constexpr int CHF = kWG * F * SU;
+  ScanTuning t;
+  t.xcd_remap = 1;
+  t.seg_chunks = std::max(4, 4 * ((k - 1 + CHF - 1) / CHF));
+  return launch_scan<T, A, C, F, SU, HS, 2, 0>(in, out, hist, nframes, k, st, t);
 }
 
 template <typename T, typename A, int C>
@@ -188,10 +200,10 @@ int dispatch_scan(int C, bool vec, bool hs, const void* in, void* out, const voi
 }
 
 // ---- direct LDS-tiled launch ---------------------------------------------------
-template <typename T, typename A, int C, int F, int U = 1>
+template <typename T, typename A, int C, int F, int U = 1, int WG = kWG>
 int launch_direct(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
                   int xcd_remap = 1) {
-  constexpr int TF = kWG * F * U;
+  constexpr int TF = WG * F * U;
   constexpr int VE = F * C;
   DirectParams p{};
   p.in = in;
@@ -203,16 +215,16 @@ int launch_direct(const void* in, void* out, const void* hist, long long nframes
   p.m = (k - 1 + F - 1) / F;
   p.off = p.m * F - (k - 1);
   p.xcd_remap = xcd_remap;
-  const size_t lds = (((size_t)(p.m + U * kWG) * VE * sizeof(T)) + 15) & ~(size_t)15;
+  const size_t lds = (((size_t)(p.m + U * WG) * VE * sizeof(T)) + 15) & ~(size_t)15;
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   const long long nblk = (nframes + TF - 1) / TF;
   if (nblk > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text), "direct<%s,acc=%s,C=%d,F=%d,U=%d> grid=%lld block=%d lds=%zu",
-             type_name<T>(), type_name<A>(), C, F, U, nblk, kWG, lds);
+             type_name<T>(), type_name<A>(), C, F, U, nblk, WG, lds);
     return MAVG_OK;
   }
-  hipLaunchKernelGGL((direct_kernel<T, A, C, F, U>), dim3((unsigned)nblk), dim3(kWG), lds, st, p);
+  hipLaunchKernelGGL((direct_kernel<T, A, C, F, U, WG>), dim3((unsigned)nblk), dim3(WG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 

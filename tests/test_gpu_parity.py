@@ -221,3 +221,31 @@ def test_sharded_split_launch_equals_whole_signal(oracle_mod, gpu, C, k, dtype):
         assert np.array_equal(y, full)
     else:
         assert_f32_close(y, full, f"C={C} k={k}")
+
+
+def test_graph_capture_and_stream_semantics(oracle_mod, gpu):
+    """mavg_run only enqueues on the caller's stream: it can be captured into a
+    HIP graph and replayed, and it runs on a non-default stream."""
+    import torch
+    import digital_signal_processsing_amd as dsp
+    n, k = 1 << 22, 1024
+    xf = oracle_mod.synth_f32(n, seed=21, dist=1)
+    ref = oracle_mod.mavg_f32(xf, k, 1)
+    x = torch.from_numpy(xf).to(gpu)
+    y = torch.empty_like(x)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        dsp.moving_average_into(x, y, k)          # warm-up on a side stream
+    s.synchronize()
+    assert_f32_close(y.cpu().numpy(), ref, "side stream")
+    y.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        dsp.moving_average_into(x, y, k)
+    g.replay()
+    torch.cuda.synchronize()
+    assert_f32_close(y.cpu().numpy(), ref, "graph replay")
+    x.copy_(torch.from_numpy(oracle_mod.synth_f32(n, seed=22, dist=1)).to(gpu))
+    g.replay()                                     # replay reads the new input in place
+    torch.cuda.synchronize()
+    assert_f32_close(y.cpu().numpy(), oracle_mod.mavg_f32(oracle_mod.synth_f32(n, seed=22, dist=1), k, 1), "replay 2")

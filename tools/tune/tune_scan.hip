@@ -110,7 +110,6 @@ int main(int argc, char** argv) {
                   return launch_scan<float, double, 1, 4, U, false, PD, NT>(x, y, nullptr, n, k, s, t);     \
                 }});
   SCAN(2, 2, 3, 1)
-  SCAN(1, 2, 1, 2)
 #define TILE(U, NT, RM)                                                                                  \
   vs.push_back({"tile U" #U " NT" #NT " remap" #RM, true, [=](hipStream_t s) {                             \
                   return launch_tile_scan<float, double, 1, 4, U, false, NT>(x, y, nullptr, n, k, s, RM);   \
@@ -119,19 +118,44 @@ int main(int argc, char** argv) {
   vs.push_back({"tileG U" #U " NT" #NT, true, [=](hipStream_t s) {                                        \
                   return launch_tile_scan<float, double, 1, 4, U, false, NT, true>(x, y, nullptr, n, k, s, 1); \
                 }});
-#define DIRECT(U, RM)                                                                                   \
-  vs.push_back({"direct U" #U " remap" #RM, true, [=](hipStream_t s) {                                     \
-                  return launch_direct<float, double, 1, 4, U>(x, y, nullptr, n, k, s, RM);                \
+#define DIRECT(U, WG)                                                                                   \
+  vs.push_back({"direct U" #U " wg" #WG, true, [=](hipStream_t s) {                                        \
+                  return launch_direct<float, double, 1, 4, U, WG>(x, y, nullptr, n, k, s, 1);             \
                 }});
-  TILE(1, 3, 1)
-  TILE(2, 0, 1)
-  TILE(4, 0, 1)
-  TILE(8, 0, 1)
-  TILE(2, 3, 1)
-  DIRECT(1, 1)
-  DIRECT(2, 1)
-  DIRECT(4, 1)
-  DIRECT(2, 0)
+#define TILEW(U, WG)                                                                                    \
+  vs.push_back({"tile U" #U " wg" #WG, true, [=](hipStream_t s) {                                         \
+                  return launch_tile_scan<float, double, 1, 4, U, false, 0, false, WG>(x, y, nullptr, n, k, s, 1); \
+                }});
+#define SEGR(U, PD, NT, SC)                                                                              \
+  vs.push_back({"seg U" #U " PD" #PD " NT" #NT " sc" #SC " remap", true, [=](hipStream_t s) {              \
+                  ScanTuning t;                                                                         \
+                  t.seg_chunks = SC;                                                                    \
+                  t.xcd_remap = 1;                                                                      \
+                  return launch_scan<float, double, 1, 4, U, false, PD, NT>(x, y, nullptr, n, k, s, t); \
+                }});
+#define TILEM(U, M)                                                                                     \
+  vs.push_back({"tile U" #U " remap" #M, true, [=](hipStream_t s) {                                       \
+                  return launch_tile_scan<float, double, 1, 4, U, false, 0, false>(x, y, nullptr, n, k, s, M); \
+                }});
+#define DIRECTM(M)                                                                                      \
+  vs.push_back({"direct U1 remap" #M, true, [=](hipStream_t s) {                                          \
+                  return launch_direct<float, double, 1, 4, 1>(x, y, nullptr, n, k, s, M);                 \
+                }});
+  TILEM(2, 1)
+  TILEM(2, 4)
+  TILEM(2, 16)
+  TILEM(2, 64)
+  TILEM(2, 256)
+  TILEM(2, 1024)
+  TILEM(8, 1)
+  TILEM(8, 16)
+  TILEM(8, 64)
+  TILEM(8, 256)
+  DIRECTM(1)
+  DIRECTM(16)
+  DIRECTM(64)
+  DIRECTM(256)
+  SEGR(2, 2, 0, 4)
 
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
