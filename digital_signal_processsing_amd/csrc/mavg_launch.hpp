@@ -14,6 +14,9 @@
 namespace mavg {
 
 constexpr int kMaxChannels = 8;
+// tile -> XCD mapping of the flat-tile kernels: runs of 64 consecutive tiles
+// per XCD, the 8 XCDs' runs adjacent (remap_tile in mavg_kernels.hpp)
+constexpr int kRemapGroup = 64;
 constexpr size_t kLdsBudget = 64 * 1024;  // per workgroup; keeps >= 2 workgroups per CU
 
 int device_cu_count();
@@ -107,7 +110,7 @@ int launch_scan(const void* in, void* out, const void* hist, long long nframes, 
 template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, bool GX = false,
           int WG = kWG>
 int launch_tile_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
-                     int xcd_remap = 1) {
+                     int xcd_remap = kRemapGroup) {
   constexpr int TF = WG * F * U;
   constexpr int NSEG = U * (WG / 64);
   constexpr int VE = F * C;
@@ -128,9 +131,9 @@ int launch_tile_scan(const void* in, void* out, const void* hist, long long nfra
   if (p.ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,gx=%d> grid=%lld block=%d lds=%zu tile_frames=%d",
+             "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,gx=%d> grid=%lld block=%d lds=%zu tile_frames=%d remap=%d",
              type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)GX, p.ntiles, WG, lds,
-             TF);
+             TF, xcd_remap);
     return MAVG_OK;
   }
   hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, GX, WG>), dim3((unsigned)p.ntiles), dim3(WG), lds, st, p);
@@ -154,10 +157,19 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
     const long long hu = (k + F - 1) / F;
     return (hu + (long long)U * kWG + 1) * kUnitBytes + (U * kNW + kNW) * C * (long long)sizeof(A);
   };
-  if (halo_bytes <= 8 * 1024 && tile_lds(2) <= (long long)kLdsBudget)
-    return launch_tile_scan<T, A, C, F, 2, HS, 0>(in, out, hist, nframes, k, st);
+  if constexpr (sizeof(T) == 2) {
+    // int16: 8 KiB tiles with non-temporal streaming for small halos, 16 KiB
+    // tiles up to an 8 KiB halo (tools/tune/tune_scan.hip ... i16)
+    if (halo_bytes <= 2 * 1024 && tile_lds(2) <= (long long)kLdsBudget)
+      return launch_tile_scan<T, A, C, F, 2, HS, kNtLoad | kNtStore>(in, out, hist, nframes, k, st, kRemapGroup);
+    if (halo_bytes <= 8 * 1024 && tile_lds(4) <= (long long)kLdsBudget)
+      return launch_tile_scan<T, A, C, F, 4, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+  } else {
+    if (halo_bytes <= 8 * 1024 && tile_lds(2) <= (long long)kLdsBudget)
+      return launch_tile_scan<T, A, C, F, 2, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+  }
   if (tile_lds(8) <= (long long)kLdsBudget)
-    return launch_tile_scan<T, A, C, F, 8, HS, 0>(in, out, hist, nframes, k, st);
+    return launch_tile_scan<T, A, C, F, 8, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
   // segment streaming: short XCD-remapped segments of at least 4 chunks and
   // 4x the pre-roll (measured 5.5-5.7 TB/s vs 5.0 for one long segment per
   // workgroup, tools/tune/tune_scan.hip)
@@ -202,7 +214,7 @@ int dispatch_scan(int C, bool vec, bool hs, const void* in, void* out, const voi
 // ---- direct LDS-tiled launch ---------------------------------------------------
 template <typename T, typename A, int C, int F, int U = 1, int WG = kWG>
 int launch_direct(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
-                  int xcd_remap = 1) {
+                  int xcd_remap = kRemapGroup) {
   constexpr int TF = WG * F * U;
   constexpr int VE = F * C;
   DirectParams p{};

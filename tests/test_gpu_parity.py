@@ -249,3 +249,21 @@ def test_graph_capture_and_stream_semantics(oracle_mod, gpu):
     g.replay()                                     # replay reads the new input in place
     torch.cuda.synchronize()
     assert_f32_close(y.cpu().numpy(), oracle_mod.mavg_f32(oracle_mod.synth_f32(n, seed=22, dist=1), k, 1), "replay 2")
+
+
+@pytest.mark.parametrize("dtype,C,k", [("f32", 1, 1024), ("i16", 1, 1024), ("i16", 2, 700), ("f32", 1, 4096),
+                                       ("i16", 1, 3000)])
+def test_grouped_xcd_remap_with_tail(oracle_mod, gpu, dtype, C, k):
+    """Tile counts just past a multiple of 8*64: the grouped tile->XCD mapping
+    covers the full groups and the tail maps to itself; every tile must be
+    written exactly once with the right halo."""
+    import digital_signal_processsing_amd as dsp
+    plan = dsp.plan(1 << 20, k, C, dsp.F32 if dtype == "f32" else dsp.I16)
+    tile = int(plan.split("tile_frames=")[1].split()[0])
+    frames = tile * (2 * 512 + 37) + 5
+    if dtype == "f32":
+        x = oracle_mod.synth_f32(frames * C, offset=99, dist=1)
+        assert_f32_close(_run(x, k, C, "auto", gpu), oracle_mod.mavg_f32(x, k, C), plan)
+    else:
+        x = oracle_mod.synth_i16(frames * C, offset=99)
+        assert np.array_equal(_run(x, k, C, "auto", gpu), oracle_mod.mavg_i16(x, k, C)), plan

@@ -74,26 +74,28 @@ struct Variant {
   unsigned long long mism = 0;
 };
 
-int main(int argc, char** argv) {
-  const int lg = argc > 1 ? atoi(argv[1]) : 30;
-  const int k = argc > 2 ? atoi(argv[2]) : 1024;
-  const int rounds = argc > 3 ? atoi(argv[3]) : 10;
+template <typename T, typename A>
+void add_variants(std::vector<struct Variant>& vs, T* x, T* y, long long n, int k);
+
+template <typename T, typename A>
+int run(int lg, int k, int rounds) {
   const long long n = 1LL << lg;
-  float *x, *y, *yref;
-  CK(hipMalloc(&x, n * 4));
-  CK(hipMalloc(&y, n * 4));
-  CK(hipMalloc(&yref, n * 4));
+  constexpr int ES = sizeof(T);
+  T *x, *y, *yref;
+  CK(hipMalloc(&x, n * ES));
+  CK(hipMalloc(&y, n * ES));
+  CK(hipMalloc(&yref, n * ES));
   unsigned long long* dcnt;
   CK(hipMalloc(&dcnt, 8));
   hipStream_t st;
   CK(hipStreamCreate(&st));
-  hipLaunchKernelGGL(synth_kernel<float>, dim3(4096), dim3(256), 0, st, x, n, (uint64_t)0x5EED, 0);
+  hipLaunchKernelGGL(synth_kernel<T>, dim3(4096), dim3(256), 0, st, x, n, (uint64_t)0x5EED, 0);
   CK(hipStreamSynchronize(st));
   int cus = device_cu_count();
-  printf("device CUs=%d n=2^%d k=%d rounds=%d\n", cus, lg, k, rounds);
+  printf("device CUs=%d n=2^%d k=%d rounds=%d dtype=%s\n", cus, lg, k, rounds, ES == 4 ? "f32" : "i16");
 
   std::vector<Variant> vs;
-  const long long n4 = n / 4;
+  const long long n4 = n * ES / 16;
   auto add_copy = [&](const char* nm, auto kern, int grid) {
     vs.push_back({nm, false, [=](hipStream_t s) {
                     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const u32x4*)x, (u32x4*)y, n4);
@@ -103,6 +105,59 @@ int main(int argc, char** argv) {
   add_copy("copy gs g16384 u2 ntLS", copy_kernel<3, 2>, 16384);
   add_copy("copy flat u1 ntLS", flat_copy<3>, (int)(n4 / 256));
 
+  add_variants<T, A>(vs, x, y, n, k);
+
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  // reference output + correctness of every scan variant
+  bool have_ref = false;
+  for (auto& v : vs) {
+    if (!v.is_scan) continue;
+    if (v.launch(st) != 0) { printf("%s: launch failed\n", v.name.c_str()); return 1; }
+    CK(hipStreamSynchronize(st));
+    if (!have_ref) {
+      CK(hipMemcpyAsync(yref, y, n * ES, hipMemcpyDeviceToDevice, st));
+      have_ref = true;
+    } else {
+      CK(hipMemsetAsync(dcnt, 0, 8, st));
+      hipLaunchKernelGGL(count_diff, dim3(2048), dim3(256), 0, st, (const uint32_t*)y, (const uint32_t*)yref,
+                         n * ES / 4, dcnt);
+      CK(hipMemcpyAsync(&v.mism, dcnt, 8, hipMemcpyDeviceToHost, st));
+    }
+    CK(hipStreamSynchronize(st));
+    CK(hipMemsetAsync(y, 0xff, n * ES, st));
+  }
+  for (auto& v : vs) { v.launch(st); v.launch(st); }
+  CK(hipStreamSynchronize(st));
+  for (int r = 0; r < rounds; ++r) {
+    for (auto& v : vs) {
+      CK(hipEventRecord(e0, st));
+      v.launch(st);
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.ms.push_back(ms);
+    }
+  }
+  printf("%-28s %9s %9s %9s %9s %s\n", "variant", "med_ms", "min_ms", "GB/s", "frac8T", "mismatch");
+  for (auto& v : vs) {
+    std::vector<float> m = v.ms;
+    std::sort(m.begin(), m.end());
+    const float med = m[m.size() / 2], mn = m[0];
+    const double gbs = 2.0 * ES * n / (med * 1e-3) / 1e9;
+    printf("%-28s %9.4f %9.4f %9.1f %9.4f %llu\n", v.name.c_str(), med, mn, gbs, gbs / 8000.0, v.mism);
+  }
+  CK(hipFree(x));
+  CK(hipFree(y));
+  CK(hipFree(yref));
+  return 0;
+}
+
+// variant lists (macros expand to launches of the library's launch helpers)
+template <>
+void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, long long n, int k) {
 #define SCAN(U, PD, NT, OV)                                                                                  \
   vs.push_back({"scan U" #U " PD" #PD " NT" #NT " ov" #OV, true, [=](hipStream_t s) {                       \
                   ScanTuning t;                                                                             \
@@ -157,46 +212,43 @@ int main(int argc, char** argv) {
   DIRECTM(256)
   SEGR(2, 2, 0, 4)
 
-  hipEvent_t e0, e1;
-  CK(hipEventCreate(&e0));
-  CK(hipEventCreate(&e1));
-  // reference output + correctness of every scan variant
-  bool have_ref = false;
-  for (auto& v : vs) {
-    if (!v.is_scan) continue;
-    if (v.launch(st) != 0) { printf("%s: launch failed\n", v.name.c_str()); return 1; }
-    CK(hipStreamSynchronize(st));
-    if (!have_ref) {
-      CK(hipMemcpyAsync(yref, y, n * 4, hipMemcpyDeviceToDevice, st));
-      have_ref = true;
-    } else {
-      CK(hipMemsetAsync(dcnt, 0, 8, st));
-      hipLaunchKernelGGL(count_diff, dim3(2048), dim3(256), 0, st, (const uint32_t*)y, (const uint32_t*)yref, n, dcnt);
-      CK(hipMemcpyAsync(&v.mism, dcnt, 8, hipMemcpyDeviceToHost, st));
-    }
-    CK(hipStreamSynchronize(st));
-    CK(hipMemsetAsync(y, 0xff, n * 4, st));
+}
+
+template <>
+void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_t* y, long long n, int k) {
+#define ITILE(U, M)                                                                                       \
+  vs.push_back({"i16 tile U" #U " remap" #M, true, [=](hipStream_t s) {                                    \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, 0, false>(x, y, nullptr, n, k, s, M); \
+                }});
+#define ITILENT(U, NT)                                                                                    \
+  vs.push_back({"i16 tile U" #U " NT" #NT, true, [=](hipStream_t s) {                                      \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, false>(x, y, nullptr, n, k, s, 1); \
+                }});
+#define IDIRECT(U)                                                                                        \
+  vs.push_back({"i16 direct U" #U, true, [=](hipStream_t s) {                                              \
+                  return launch_direct<int16_t, int32_t, 1, 8, U>(x, y, nullptr, n, k, s, 1);               \
+                }});
+  ITILE(1, 1)
+  ITILE(2, 1)
+  ITILE(4, 1)
+  ITILE(8, 1)
+  ITILE(2, 64)
+  ITILE(4, 64)
+  ITILENT(1, 3)
+  ITILENT(2, 3)
+  ITILENT(4, 3)
+  ITILENT(2, 1)
+  ITILENT(4, 2)
+  if (k <= 64) {
+    IDIRECT(1)
+    IDIRECT(2)
   }
-  for (auto& v : vs) { v.launch(st); v.launch(st); }
-  CK(hipStreamSynchronize(st));
-  for (int r = 0; r < rounds; ++r) {
-    for (auto& v : vs) {
-      CK(hipEventRecord(e0, st));
-      v.launch(st);
-      CK(hipEventRecord(e1, st));
-      CK(hipEventSynchronize(e1));
-      float ms;
-      CK(hipEventElapsedTime(&ms, e0, e1));
-      v.ms.push_back(ms);
-    }
-  }
-  printf("%-28s %9s %9s %9s %9s %s\n", "variant", "med_ms", "min_ms", "GB/s", "frac8T", "mismatch");
-  for (auto& v : vs) {
-    std::vector<float> m = v.ms;
-    std::sort(m.begin(), m.end());
-    const float med = m[m.size() / 2], mn = m[0];
-    const double gbs = 8.0 * n / (med * 1e-3) / 1e9;
-    printf("%-28s %9.4f %9.4f %9.1f %9.4f %llu\n", v.name.c_str(), med, mn, gbs, gbs / 8000.0, v.mism);
-  }
-  return 0;
+}
+
+int main(int argc, char** argv) {
+  const int lg = argc > 1 ? atoi(argv[1]) : 30;
+  const int k = argc > 2 ? atoi(argv[2]) : 1024;
+  const int rounds = argc > 3 ? atoi(argv[3]) : 10;
+  const std::string dt = argc > 4 ? argv[4] : "f32";
+  return dt == "i16" ? run<int16_t, int32_t>(lg, k, rounds) : run<float, double>(lg, k, rounds);
 }
