@@ -158,10 +158,10 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
     return (hu + (long long)U * kWG + 1) * kUnitBytes + (U * kNW + kNW) * C * (long long)sizeof(A);
   };
   if constexpr (sizeof(T) == 2) {
-    // int16: 8 KiB tiles with non-temporal streaming for small halos, 16 KiB
-    // tiles up to an 8 KiB halo (tools/tune/tune_scan.hip ... i16)
-    if (halo_bytes <= 2 * 1024 && tile_lds(2) <= (long long)kLdsBudget)
-      return launch_tile_scan<T, A, C, F, 2, HS, kNtLoad | kNtStore>(in, out, hist, nframes, k, st, kRemapGroup);
+    // int16: 16 KiB tiles, non-temporal streaming for small halos
+    // (tools/tune/tune_scan.hip ... i16, back-to-back bursts)
+    if (halo_bytes <= 2 * 1024 && tile_lds(4) <= (long long)kLdsBudget)
+      return launch_tile_scan<T, A, C, F, 4, HS, kNtLoad | kNtStore>(in, out, hist, nframes, k, st, kRemapGroup);
     if (halo_bytes <= 8 * 1024 && tile_lds(4) <= (long long)kLdsBudget)
       return launch_tile_scan<T, A, C, F, 4, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
   } else {

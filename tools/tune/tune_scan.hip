@@ -77,6 +77,8 @@ struct Variant {
 template <typename T, typename A>
 void add_variants(std::vector<struct Variant>& vs, T* x, T* y, long long n, int k);
 
+static int g_burst = 1;  // launches per timed sample (back-to-back, like bench.py's steps)
+
 template <typename T, typename A>
 int run(int lg, int k, int rounds) {
   const long long n = 1LL << lg;
@@ -133,12 +135,12 @@ int run(int lg, int k, int rounds) {
   for (int r = 0; r < rounds; ++r) {
     for (auto& v : vs) {
       CK(hipEventRecord(e0, st));
-      v.launch(st);
+      for (int b = 0; b < g_burst; ++b) v.launch(st);
       CK(hipEventRecord(e1, st));
       CK(hipEventSynchronize(e1));
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
-      v.ms.push_back(ms);
+      v.ms.push_back(ms / g_burst);
     }
   }
   printf("%-28s %9s %9s %9s %9s %s\n", "variant", "med_ms", "min_ms", "GB/s", "frac8T", "mismatch");
@@ -224,21 +226,27 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   vs.push_back({"i16 tile U" #U " NT" #NT, true, [=](hipStream_t s) {                                      \
                   return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, false>(x, y, nullptr, n, k, s, 1); \
                 }});
+#define ITILENTR(U, NT, M)                                                                                \
+  vs.push_back({"i16 tile U" #U " NT" #NT " remap" #M, true, [=](hipStream_t s) {                          \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, false>(x, y, nullptr, n, k, s, M); \
+                }});
+#define IPROD()                                                                                           \
+  vs.push_back({"i16 product mavg_run", true, [=](hipStream_t s) {                                        \
+                  return mavg_run(x, y, n, 1, k, MAVG_I16, MAVG_ALGO_AUTO, 0, nullptr, nullptr, 0, s);       \
+                }});
 #define IDIRECT(U)                                                                                        \
   vs.push_back({"i16 direct U" #U, true, [=](hipStream_t s) {                                              \
                   return launch_direct<int16_t, int32_t, 1, 8, U>(x, y, nullptr, n, k, s, 1);               \
                 }});
-  ITILE(1, 1)
   ITILE(2, 1)
-  ITILE(4, 1)
-  ITILE(8, 1)
-  ITILE(2, 64)
   ITILE(4, 64)
-  ITILENT(1, 3)
   ITILENT(2, 3)
-  ITILENT(4, 3)
-  ITILENT(2, 1)
-  ITILENT(4, 2)
+  ITILENTR(2, 3, 64)
+  ITILENTR(2, 3, 16)
+  ITILENTR(2, 3, 256)
+  ITILENTR(4, 3, 64)
+  ITILENTR(2, 3, 0)
+  IPROD()
   if (k <= 64) {
     IDIRECT(1)
     IDIRECT(2)
@@ -250,5 +258,7 @@ int main(int argc, char** argv) {
   const int k = argc > 2 ? atoi(argv[2]) : 1024;
   const int rounds = argc > 3 ? atoi(argv[3]) : 10;
   const std::string dt = argc > 4 ? argv[4] : "f32";
+  g_burst = argc > 5 ? atoi(argv[5]) : 1;
+  printf("burst=%d (launches per timed sample)\n", g_burst);
   return dt == "i16" ? run<int16_t, int32_t>(lg, k, rounds) : run<float, double>(lg, k, rounds);
 }
