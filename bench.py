@@ -55,6 +55,12 @@ def parse():
     ap.add_argument("--cpu-samples", type=int, default=1 << 28, help="bounded CPU-baseline sample (samples)")
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the measured path); gloo = rehearsal of the N>1 orchestration on a "
+                         "box with fewer GPUs than ranks (halo staged through host memory, ranks share GPUs)")
+    ap.add_argument("--check", action="store_true",
+                    help="after timing, every rank checks sampled output slices (incl. its shard head) "
+                         "against the CPU oracle")
     ap.add_argument("--all-workloads", action="store_true",
                     help="print one extra JSON line per secondary workload (rank 0, N=1 only)")
     return ap.parse_args()
@@ -70,10 +76,15 @@ def init_dist(args):
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dist_backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     return rank, world, local
 
 
@@ -91,7 +102,8 @@ def max_over_ranks(v: float, world: int) -> float:
     import torch.distributed as dist
     if world == 1:
         return v
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -129,6 +141,35 @@ def cpu_baseline(args, n_total, k, C, seed):
         "sample": f"{n} fp32 samples (first {n} of the benchmark's synthetic stream), k={k}, C={C}, "
                   f"median of {args.cpu_reps} reps, {med * 1e3:.1f} ms/rep, single thread",
     }
+
+
+def check_output(y, n, k, C, dt, seed, rank, samples=64, span=4096):
+    """Compare slices of this rank's output shard with the oracle run on the
+    same global synthetic stream (test leg: the oracle is only the checker)."""
+    import numpy as np
+    import oracle
+    oracle.build()
+    frames = n // C
+    f_base = rank * frames                       # global frame of local frame 0
+    rng = np.random.default_rng(rank)
+    starts = [0, max(0, frames - span)] + list(rng.integers(0, max(1, frames - span), samples))
+    ycpu = y.cpu().numpy()
+    bad = 0
+    for s in starts:
+        s = int(s)
+        e = min(frames, s + span)
+        g0 = max(0, f_base + s - (k - 1))            # first global frame the window needs
+        cnt = (f_base + e - g0) * C
+        if dt == "f32":
+            xs = oracle.synth_f32(cnt, seed=seed, offset=g0 * C)
+            ref = oracle.mavg_f32(xs, k, C)[(f_base + s - g0) * C:]
+            got = ycpu[s * C:e * C].astype(np.float64)
+            bad += int(np.sum(np.abs(got - ref) > 1e-5 * np.maximum(np.abs(ref), 1e-30)))
+        else:
+            xs = oracle.synth_i16(cnt, seed=seed, offset=g0 * C)
+            ref = oracle.mavg_i16(xs, k, C)[(f_base + s - g0) * C:]
+            bad += int(np.sum(ycpu[s * C:e * C] != ref))
+    return {"slices": len(starts), "span_frames": span, "mismatches": bad}
 
 
 def run_workload(args, name, rank, world, with_cpu):
@@ -221,6 +262,15 @@ def run_workload(args, name, rank, world, with_cpu):
             "algorithmic_bytes_per_launch": alg_bytes,
         },
     }
+    if args.check:
+        res = check_output(y, n, k, C, dt, seed, rank)
+        if world > 1:
+            import torch.distributed as dist
+            allres = [None] * world
+            dist.all_gather_object(allres, res)
+            res = {"ranks": world, "slices": sum(r["slices"] for r in allres),
+                   "mismatches": sum(r["mismatches"] for r in allres)}
+        line["check"] = res
     if with_cpu and rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, n, k, C, seed)
     del x, y

@@ -49,16 +49,37 @@ def start_halo_exchange(x_local, grade: int, channels: int = 1, group=None, recv
         return [], None
     if x_local.numel() < h:
         raise ValueError(f"shard holds {x_local.numel()} samples < halo {h}: use fewer ranks or a smaller grade")
+    # gloo cannot move device tensors: stage the halo through host memory
+    # (rehearsal / CPU-only use; the measured multi-GPU path is NCCL = RCCL)
+    staged = x_local.is_cuda and dist.get_backend(group) != "nccl"
     ops = []
     if rank + 1 < world:
         tail = x_local[x_local.numel() - h:]
+        if staged:
+            tail = tail.cpu()
         ops.append(dist.P2POp(dist.isend, tail, _peer(rank + 1, group), group))
     hist = None
+    wire = None
     if rank > 0:
         hist = recv_buf if recv_buf is not None else torch.empty(h, dtype=x_local.dtype, device=x_local.device)
-        ops.append(dist.P2POp(dist.irecv, hist, _peer(rank - 1, group), group))
+        wire = torch.empty(h, dtype=x_local.dtype) if staged else hist
+        ops.append(dist.P2POp(dist.irecv, wire, _peer(rank - 1, group), group))
     reqs = dist.batch_isend_irecv(ops) if ops else []
+    if staged and wire is not None:
+        reqs = [_StagedRecv(reqs, wire, hist)]
     return reqs, hist
+
+
+class _StagedRecv:
+    """Completes the host-staged receive: wait, then copy the halo to the device."""
+
+    def __init__(self, reqs, wire, dst):
+        self.reqs, self.wire, self.dst = reqs, wire, dst
+
+    def wait(self):
+        for r in self.reqs:
+            r.wait()
+        self.dst.copy_(self.wire)
 
 
 def exchange_halo(x_local, grade: int, channels: int = 1, group=None, recv_buf=None):

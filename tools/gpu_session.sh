@@ -35,6 +35,11 @@ for step in "$@"; do
             python bench.py --steps 5 --warmup 2 --no-cpu-baseline --all-workloads &&
          run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
             python bench.py --steps 5 --warmup 2 --no-cpu-baseline --all-workloads ;;
+    check) run check1 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --check --all-workloads ;;
+    dist) run dist2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+            --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --check &&
+          run dist4 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+            --master-port 29512 bench.py --gpus 4 --steps 3 --warmup 1 --dist-backend gloo --check ;;
     *) echo "unknown step $step" ;;
   esac
 done
