@@ -262,26 +262,25 @@ struct ScanParams {
   OutParams o;
 };
 
-// bijective remap: blocks b and b+8 share an XCD (observed round-robin
-// dispatch, cdna_hip_programming.md 5.5 T1); give each XCD a contiguous run.
-__device__ __forceinline__ long long xcd_contiguous(long long b, long long nb) {
-  const long long q = nb / 8, r = nb % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-// grouped remap: every XCD takes runs of G consecutive tiles and the eight
-// XCDs' runs are adjacent, so the whole chip works inside one window of 8*G
-// tiles (tail blocks beyond the last full group map to themselves).
-__device__ __forceinline__ long long xcd_grouped(long long b, long long nb, long long G) {
-  const long long full = nb / (8 * G) * (8 * G);
-  if (b >= full) return b;
-  const long long i = b / 8, x = b % 8;
-  return (i / G) * (8 * G) + x * G + (i % G);
-}
-// remap mode: 0 identity, 1 contiguous run per XCD, G > 1: grouped with G tiles
-__device__ __forceinline__ long long remap_tile(long long b, long long nb, int mode) {
+// Tile -> workgroup remaps (speed only, never correctness: blocks b and b+8
+// share an XCD under the observed round-robin dispatch, cdna_hip_programming.md
+// 5.5 T1).  32-bit scalar arithmetic only (the grid is < 2^31 workgroups):
+// a 64-bit divide here costs ~150 SALU instructions per wave.
+// mode 0: identity; 1: each XCD takes one contiguous run of nb/8 tiles
+// (bijective for any nb); G = 2^g > 1: each XCD takes runs of G consecutive
+// tiles and the 8 XCDs' runs are adjacent, so the whole chip works inside a
+// window of 8G tiles; blocks past the last full group of 8G map to themselves.
+__device__ __forceinline__ long long remap_tile(unsigned b, unsigned nb, int mode) {
   if (mode == 0) return b;
-  if (mode == 1) return xcd_contiguous(b, nb);
-  return xcd_grouped(b, nb, mode);
+  if (mode == 1) {
+    const unsigned q = nb >> 3, r = nb & 7u, x = b & 7u;
+    return (long long)((x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3));
+  }
+  const unsigned g = (unsigned)__builtin_ctz((unsigned)mode);  // mode = G, a power of two
+  const unsigned full = nb & ~((8u << g) - 1u);
+  if (b >= full) return b;
+  const unsigned i = b >> 3, x = b & 7u;
+  return (long long)(((i >> g) << (g + 3)) + (x << g) + (i & ((1u << g) - 1u)));
 }
 
 // T: sample type; A: accumulator; C: channels; F: frames per lane unit;

@@ -78,6 +78,19 @@ template <typename T, typename A>
 void add_variants(std::vector<struct Variant>& vs, T* x, T* y, long long n, int k);
 
 static int g_burst = 1;  // launches per timed sample (back-to-back, like bench.py's steps)
+static std::string g_filter;  // "a|b": keep only variants whose name contains a or b
+
+static bool keep(const std::string& name) {
+  if (g_filter.empty()) return true;
+  size_t st = 0;
+  while (st <= g_filter.size()) {
+    size_t e = g_filter.find('|', st);
+    if (e == std::string::npos) e = g_filter.size();
+    if (name.find(g_filter.substr(st, e - st)) != std::string::npos) return true;
+    st = e + 1;
+  }
+  return false;
+}
 
 template <typename T, typename A>
 int run(int lg, int k, int rounds) {
@@ -108,6 +121,12 @@ int run(int lg, int k, int rounds) {
   add_copy("copy flat u1 ntLS", flat_copy<3>, (int)(n4 / 256));
 
   add_variants<T, A>(vs, x, y, n, k);
+  {
+    std::vector<Variant> kept;
+    for (auto& v : vs)
+      if (keep(v.name)) kept.push_back(v);
+    vs.swap(kept);
+  }
 
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -259,6 +278,7 @@ int main(int argc, char** argv) {
   const int rounds = argc > 3 ? atoi(argv[3]) : 10;
   const std::string dt = argc > 4 ? argv[4] : "f32";
   g_burst = argc > 5 ? atoi(argv[5]) : 1;
+  g_filter = argc > 6 ? argv[6] : "";
   printf("burst=%d (launches per timed sample)\n", g_burst);
   return dt == "i16" ? run<int16_t, int32_t>(lg, k, rounds) : run<float, double>(lg, k, rounds);
 }
