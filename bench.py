@@ -53,7 +53,9 @@ def parse():
     ap.add_argument("--algo", default=None, help="override the workload's algorithm")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-samples", type=int, default=1 << 28, help="bounded CPU-baseline sample (samples)")
-    ap.add_argument("--cpu-reps", type=int, default=5)
+    ap.add_argument("--cpu-reps", type=int, default=10)
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0),
+                    help="threads of the multi-core CPU baseline (default: OMP_NUM_THREADS, else os.cpu_count())")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the measured path); gloo = rehearsal of the N>1 orchestration on a "
@@ -133,7 +135,23 @@ def cpu_baseline(args, n_total, k, C, seed):
         oracle.mavg_f32(x, k, C)
         times.append(time.perf_counter() - t)
     med = statistics.median(times)
-    return {
+    threads = args.cpu_threads or os.cpu_count() or 1
+    oracle.mavg_f32_mt(x[: min(n, 1 << 20)], k, C, threads)
+    mt = []
+    for _ in range(max(3, args.cpu_reps // 2)):
+        t = time.perf_counter()
+        oracle.mavg_f32_mt(x, k, C, threads)
+        mt.append(time.perf_counter() - t)
+    mt_med = statistics.median(mt)
+    multicore = {
+        "value": round(n / mt_med / 1e9, 4),
+        "unit": "Gsamples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"same sample, OpenMP chunks with a k-frame halo each, {threads} threads, "
+                  f"median of {len(mt)} reps, {mt_med * 1e3:.1f} ms/rep",
+    }
+    single = {
         "value": round(n / med / 1e9, 4),
         "unit": "Gsamples/s",
         "cores": 1,
@@ -141,6 +159,7 @@ def cpu_baseline(args, n_total, k, C, seed):
         "sample": f"{n} fp32 samples (first {n} of the benchmark's synthetic stream), k={k}, C={C}, "
                   f"median of {args.cpu_reps} reps, {med * 1e3:.1f} ms/rep, single thread",
     }
+    return single, multicore
 
 
 def check_output(y, n, k, C, dt, seed, rank, samples=64, span=4096):
@@ -272,7 +291,7 @@ def run_workload(args, name, rank, world, with_cpu):
                    "mismatches": sum(r["mismatches"] for r in allres)}
         line["check"] = res
     if with_cpu and rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args, n, k, C, seed)
+        line["cpu_baseline"], line["cpu_baseline_multicore"] = cpu_baseline(args, n, k, C, seed)
     del x, y
     torch.cuda.empty_cache()
     return line

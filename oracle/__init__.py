@@ -42,6 +42,8 @@ def _load():
     lib.oracle_mavg_i16.argtypes = [p, p, sz, i, i]
     lib.oracle_mavg_f32.argtypes = [p, p, sz, i, i]
     lib.oracle_window_sum_i64.argtypes = [p, sz, i, i, sz, sz, p]
+    lib.oracle_mavg_f32_mt.argtypes = [p, p, sz, i, i, i]
+    lib.oracle_mavg_f32_mt.restype = ctypes.c_int
     lib.oracle_synth_i16.argtypes = [p, sz, u64, u64]
     lib.oracle_synth_f32.argtypes = [p, sz, u64, u64, i]
     for f in (lib.oracle_mavg_i16, lib.oracle_mavg_f32, lib.oracle_window_sum_i64):
@@ -73,6 +75,16 @@ def mavg_f32(x: np.ndarray, k: int, channels: int = 1) -> np.ndarray:
     rc = _load().oracle_mavg_f32(_ptr(x), _ptr(y), x.size, channels, k)
     if rc != 0:
         raise ValueError(f"oracle_mavg_f32: bad arguments (n={x.size}, C={channels}, k={k})")
+    return y
+
+
+def mavg_f32_mt(x: np.ndarray, k: int, channels: int = 1, threads: int = 8) -> np.ndarray:
+    """Multi-core CPU baseline (OpenMP, per-chunk k-frame halo)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.zeros_like(x)
+    rc = _load().oracle_mavg_f32_mt(_ptr(x), _ptr(y), x.size, channels, k, threads)
+    if rc != 0:
+        raise ValueError("oracle_mavg_f32_mt: bad arguments")
     return y
 
 

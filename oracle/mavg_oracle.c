@@ -131,3 +131,39 @@ void oracle_synth_f32(float* x, size_t n, uint64_t seed, uint64_t offset, int di
         else           x[i] = (float)(int16_t)(uint16_t)(h >> 48);
     }
 }
+
+/* ---- multi-core CPU baseline --------------------------
+ * Same arithmetic as oracle_mavg_f32, split into `threads` contiguous frame
+ * chunks; each chunk seeds its running sums from the k frames before it
+ * (the CPU analogue of the GPU tiles' halo).  Results equal the serial loop
+ * up to fp64 summation order.  Reported beside the single-core baseline,
+ * never used as a checker. */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+int oracle_mavg_f32_mt(const float* x, float* y, size_t n, int C, int k, int threads)
+{
+    if (C < 1 || C > ORACLE_MAX_CH || k < 1 || (n % (size_t)C) != 0 || threads < 1) return -1;
+    const size_t frames = n / (size_t)C;
+    const double dk = (double)k;
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (int t = 0; t < threads; ++t) {
+        const size_t f0 = frames * (size_t)t / (size_t)threads;
+        const size_t f1 = frames * (size_t)(t + 1) / (size_t)threads;
+        double sum[ORACLE_MAX_CH];
+        for (int ch = 0; ch < C; ++ch) {
+            double s = 0.0;
+            /* the k frames before f0: the first step below subtracts x[f0-k] */
+            const size_t lo = f0 > (size_t)k ? f0 - (size_t)k : 0;
+            for (size_t j = lo; j < f0; ++j) s += (double)x[j * C + ch];
+            sum[ch] = s;
+        }
+        for (size_t i = f0; i < f1; ++i)
+            for (int ch = 0; ch < C; ++ch) {
+                sum[ch] += (double)x[i * C + ch];
+                if (i >= (size_t)k) sum[ch] -= (double)x[(i - (size_t)k) * C + ch];
+                y[i * C + ch] = (float)(sum[ch] / dk);
+            }
+    }
+    return 0;
+}

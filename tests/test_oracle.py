@@ -105,3 +105,10 @@ def test_golden_fixtures(oracle_mod):
     digests = dict(line.split() for line in open(os.path.join(GOLDEN, "digests.txt")))
     x = oracle_mod.synth_i16(1 << 20, seed=0x5EED)
     assert hashlib.sha256(oracle_mod.mavg_i16(x, 32, 1).tobytes()).hexdigest() == digests["i16_n1048576_C1_k32"]
+
+
+@pytest.mark.parametrize("C,k,threads", [(1, 1024, 8), (2, 7, 3), (1, 1, 4), (3, 5000, 16), (1, 64, 1)])
+def test_multicore_baseline_equals_serial(oracle_mod, C, k, threads):
+    x = oracle_mod.synth_f32(200_003 * C, offset=k, dist=1)
+    np.testing.assert_allclose(oracle_mod.mavg_f32_mt(x, k, C, threads), oracle_mod.mavg_f32(x, k, C),
+                               rtol=1e-6, atol=1e-7)
