@@ -683,10 +683,39 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   }
 
   // ---- d = x - x[n-k]; in-lane, wave and segment scans ----
+  // Hillis-Steele flavour (LDS-staged): transposed ownership, lane l holds
+  // frames l, l+64, ..., l+64(F-1) of its 64F-frame wave segment, so every
+  // register holds 64 consecutive frames and the log-step scan runs on DPP
+  // (6 steps per element, O(n log n) work) with a scalar carry across the F
+  // registers; x and x[n-k] both come from the LDS stage.
+  constexpr bool kHsT = HS && !GX;
   A v[U][F][C];
   A lx[U][C];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
+    if constexpr (kHsT) {
+      const int sb = (u * WG + w * 64) * F;  // tile-local first frame of this wave segment
+      A run[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) run[c] = (A)0;
+#pragma unroll
+      for (int r = 0; r < F; ++r) {
+        const int fl = sb + r * 64 + lane;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const A d = to_acc<A>(stage[(Ha + fl) * C + c]) - to_acc<A>(stage[(Ha + fl - k) * C + c]);
+          const A incl = wave_incl_scan(d);
+          v[u][r][c] = incl + run[c];
+          run[c] += readlane(incl, 63);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        lx[u][c] = (A)0;
+        if (lane == 0) tot[(u * NW + w) * C + c] = run[c];
+      }
+      continue;
+    }
     const int j = u * WG + tid;
     const int e = (Ha + j * F - k) * C;      // LDS element of x[n-k]
     U_t xk;
@@ -804,6 +833,17 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
     }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
+    if constexpr (kHsT) {
+      const long long sb = t0 + (long long)(u * WG + w * 64) * F;
+#pragma unroll
+      for (int r = 0; r < F; ++r) {
+        const long long f = sb + r * 64 + lane;
+        if (tile_full || f < nframes)
+#pragma unroll
+          for (int c = 0; c < C; ++c) out[f * C + c] = to_out<T, A>(base[u][c] + v[u][r][c], p.o);
+      }
+      continue;
+    }
     const long long f = t0 + (long long)(u * WG + tid) * F;
     U_t y;
 #pragma unroll

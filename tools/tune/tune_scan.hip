@@ -217,6 +217,12 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   vs.push_back({"direct U1 remap" #M, true, [=](hipStream_t s) {                                          \
                   return launch_direct<float, double, 1, 4, 1>(x, y, nullptr, n, k, s, M);                 \
                 }});
+  vs.push_back({"hillis tile U2", true, [=](hipStream_t s) {
+                  return launch_tile_scan<float, double, 1, 4, 2, true, 0, false>(x, y, nullptr, n, k, s);
+                }});
+  vs.push_back({"hillis tile U1", true, [=](hipStream_t s) {
+                  return launch_tile_scan<float, double, 1, 4, 1, true, 0, false>(x, y, nullptr, n, k, s);
+                }});
   TILEM(2, 1)
   TILEM(2, 4)
   TILEM(2, 16)
