@@ -257,6 +257,7 @@ def run_workload(args, name, rank, world, with_cpu):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": dt,
+        "accumulate": "f64" if dt == "f32" else ("i32" if k <= 65535 else "i64"),
         "data": "synthetic (device counter-based splitmix64, int16-valued samples)",
         "config": {
             "workload": f"{name}: {n} {dt} samples per GPU, k={k}, C={C}, algo={resolved}",

@@ -41,6 +41,7 @@ inline std::string read_wav_i16(const std::string& path, WavInfo& info, std::vec
     const uint32_t size = rd32(ch + 4);
     if (std::memcmp(ch, "fmt ", 4) == 0) {
       if (size < 16) return "fmt chunk too short";
+      if (size > (1u << 20)) return "fmt chunk too large";
       std::vector<unsigned char> f(size);
       if (!in.read(reinterpret_cast<char*>(f.data()), size)) return "truncated fmt chunk";
       format = rd16(f.data());
@@ -55,6 +56,12 @@ inline std::string read_wav_i16(const std::string& path, WavInfo& info, std::vec
       if (format != 1 && format != 0xFFFE) return "not integer PCM (format " + std::to_string(format) + ")";
       if (info.channels == 0) return "zero channels";
       info.data_bytes = size;
+      // never allocate more than the file holds (a corrupt size field)
+      const std::streampos here = in.tellg();
+      in.seekg(0, std::ios::end);
+      const std::streamoff remaining = in.tellg() - here;
+      in.seekg(here);
+      if (remaining < (std::streamoff)size) return "truncated data chunk";
       samples.resize(size / 2);
       if (!in.read(reinterpret_cast<char*>(samples.data()), (std::streamsize)(samples.size() * 2)))
         return "truncated data chunk";

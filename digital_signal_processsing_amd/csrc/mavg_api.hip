@@ -41,7 +41,7 @@ int validate(size_t n, int C, int k, int dtype, int algo) {
   if (algo < MAVG_ALGO_AUTO || algo > MAVG_ALGO_NAIVE) return MAVG_ERR_INVALID_ARG;
   if (C < 1 || k < 1) return MAVG_ERR_INVALID_ARG;
   if (n % (size_t)C != 0) return MAVG_ERR_INVALID_ARG;
-  if (C > kMaxChannels) return MAVG_ERR_UNSUPPORTED;
+  if (C > kMaxChannels && algo != MAVG_ALGO_AUTO && algo != MAVG_ALGO_NAIVE) return MAVG_ERR_UNSUPPORTED;
   if (n / (size_t)C > (size_t)0x3fffffffffffffffULL) return MAVG_ERR_UNSUPPORTED;
   return MAVG_OK;
 }
@@ -84,11 +84,12 @@ const char* mavg_algo_name(int algo) {
 // 6.27 TB/s at k=7 vs 6.18 for the tile scan), the flat-tile Blelloch scan
 // otherwise (O(1) per output for any k).  Both move 1.00x the algorithmic
 // bytes on HBM (profiles/).
+// More than kMaxChannels channels: only the naive kernel (runtime C) applies.
 int mavg_resolve_algo(size_t n_samples, int channels, int grade, int dtype, int algo) {
   (void)n_samples;
-  (void)channels;
   (void)dtype;
   if (algo != MAVG_ALGO_AUTO) return algo;
+  if (channels > kMaxChannels) return MAVG_ALGO_NAIVE;
   return grade <= 9 ? MAVG_ALGO_DIRECT : MAVG_ALGO_BLELLOCH;
 }
 

@@ -47,10 +47,6 @@ constexpr int kNW = kWG / 64;     // waves per workgroup
 // ----------------------------------------------------------------------------
 // small helpers
 // ----------------------------------------------------------------------------
-template <typename T> struct AccFor;
-template <> struct AccFor<float> { using type = double; };
-template <> struct AccFor<int16_t> { using type = int32_t; };
-
 template <typename A> __device__ __forceinline__ A to_acc(float x) { return (A)x; }
 template <typename A> __device__ __forceinline__ A to_acc(int16_t x) { return (A)x; }
 

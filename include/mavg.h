@@ -70,7 +70,7 @@ typedef enum {
 typedef enum {
     MAVG_OK = 0,
     MAVG_ERR_INVALID_ARG = 1, /* null pointer, k < 1, C < 1, n not a multiple of C, bad enum */
-    MAVG_ERR_UNSUPPORTED = 2, /* valid but not implemented (e.g. C > 8, k too large for algo) */
+    MAVG_ERR_UNSUPPORTED = 2, /* valid but not implemented (C > 8 outside AUTO/NAIVE, k too large for algo) */
     MAVG_ERR_MISALIGNED = 3,  /* a 16-B-unit algorithm got a pointer not 16-B aligned */
     MAVG_ERR_WORKSPACE = 4,   /* ws_bytes smaller than mavg_workspace_bytes() */
     MAVG_ERR_HIP = 5          /* a HIP runtime call or kernel launch failed */
@@ -85,9 +85,9 @@ int mavg_workspace_bytes(size_t n_samples, int channels, int grade, int dtype,
  *   d_history  NULL (zero history) or (grade-1)*channels samples that
  *              precede d_in (any alignment).
  *   block_size the reference's argv block size (multiple of 32 in
- *              [32, 1024]); kernels use it rounded up to a multiple of the
- *              64-lane wavefront where the algorithm takes a block size,
- *              0 = the algorithm's tuned default.
+ *              [32, 1024]) or 0; accepted for drop-in compatibility (the
+ *              CLIs log it), while every MI355X kernel uses its tuned
+ *              256-thread (4 x wave64) workgroup.
  *   stream     hipStream_t or NULL.
  * Returns a mavg_status.  Nothing is enqueued unless MAVG_OK is returned
  * (MAVG_ERR_HIP excepted, when the launch itself failed).

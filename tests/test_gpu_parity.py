@@ -267,3 +267,14 @@ def test_grouped_xcd_remap_with_tail(oracle_mod, gpu, dtype, C, k):
     else:
         x = oracle_mod.synth_i16(frames * C, offset=99)
         assert np.array_equal(_run(x, k, C, "auto", gpu), oracle_mod.mavg_i16(x, k, C)), plan
+
+
+def test_many_channels_auto(oracle_mod, gpu):
+    """C > 8 (beyond the templated kernels): AUTO runs the naive any-C kernel."""
+    for C, dtype in ((12, "i16"), (16, "f32")):
+        if dtype == "i16":
+            x = oracle_mod.synth_i16(3001 * C, offset=C)
+            assert np.array_equal(_run(x, 37, C, "auto", gpu), oracle_mod.mavg_i16(x, 37, C))
+        else:
+            x = oracle_mod.synth_f32(3001 * C, offset=C, dist=1)
+            assert_f32_close(_run(x, 37, C, "auto", gpu), oracle_mod.mavg_f32(x, 37, C), "C=16")
