@@ -7,8 +7,11 @@ collected in SEPARATE --pmc passes (they do not fit one pass); both are in
 KiB; on gfx950 FETCH_SIZE reports exactly half of the bytes of a wide
 (16 B/lane) coalesced streaming read, so it is doubled; WRITE_SIZE is exact
 for 16-B streaming stores.  hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024.
-Dispatches are matched to workloads by kernel family and grid size, the grid
-being the one mavg_plan() reports for that workload (no GPU needed here).
+Dispatches are matched to workloads by the kernel's full template signature
+and grid size, both rebuilt from the plan string mavg_plan() reports for that
+workload (no GPU needed here).  Several workloads share a grid (carry_2p30 and
+both int16 lines launch 131072 workgroups), so the family and grid alone are
+not enough.
 
     python tools/pmc_traffic.py <fetch.csv> <write.csv> <out.json>
 """
@@ -23,14 +26,49 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+TYPE = {"f32": "float", "f64": "double", "i16": "short", "i32": "int", "i64": "long"}
+FAMILY = {"tile_scan": "tile_scan_kernel", "segment_scan": "scan_kernel", "direct": "direct_kernel",
+          "naive": "naive_kernel"}
+
+
+def kernel_key(name):
+    """'void mavg::tile_scan_kernel<float, double, 1, 4, 8, false, 0, false, 256>(...)'
+    -> ('tile_scan_kernel', ('float', 'double', '1', ...))"""
+    m = re.match(r"^void mavg::(\w+)<([^>]*)>", name)
+    if not m:
+        return None
+    return m.group(1), tuple(a.strip() for a in m.group(2).split(","))
+
+
+def plan_key(plan):
+    """The kernel_key() a launch with this mavg_plan() string produces."""
+    fam, rest = plan.split("<", 1)
+    fields = rest.split(">", 1)[0].split(",")
+    T, acc = TYPE[fields[0]], TYPE[fields[1].split("=")[1]]
+    kv = dict(f.split("=") for f in fields[2:] if "=" in f)
+    flavour = [f for f in fields[2:] if "=" not in f]
+    hs = "true" if flavour and flavour[0] == "hillis" else "false"
+    wg = re.search(r"block=(\d+)", plan).group(1)
+    if fam == "tile_scan":
+        args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["nt"], "true" if kv["gx"] == "1" else "false", wg)
+    elif fam == "direct":
+        args = (T, acc, kv["C"], kv["F"], kv["U"], wg)
+    elif fam == "segment_scan":
+        args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["pd"], kv["nt"])
+    else:
+        args = (T, acc)
+    return FAMILY[fam], args
+
+
 def per_kernel(path, counter):
     out = {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        fam = re.sub(r"^void mavg::(\w+)<.*", r"\1", r["Kernel_Name"])
-        key = (fam, int(r["Grid_Size"]))
-        out.setdefault(key, []).append(float(r["Counter_Value"]))
+        kk = kernel_key(r["Kernel_Name"])
+        if kk is None:
+            continue
+        out.setdefault((kk, int(r["Grid_Size"])), []).append(float(r["Counter_Value"]))
     return out
 
 
@@ -39,15 +77,13 @@ def main(fetch_csv, write_csv, out_json):
     import digital_signal_processsing_amd as dsp
     fetch = per_kernel(fetch_csv, "FETCH_SIZE")
     write = per_kernel(write_csv, "WRITE_SIZE")
-    fam_of = {"tile_scan": "tile_scan_kernel", "segment_scan": "scan_kernel", "direct": "direct_kernel",
-              "naive": "naive_kernel"}
     result = {}
     for name, (n, k, C, dt, algo) in bench.WORKLOADS.items():
         dtc = dsp.F32 if dt == "f32" else dsp.I16
         plan = dsp.plan(n, k, C, dtc, algo)
         grid = int(re.search(r"grid=(\d+)", plan).group(1)) * int(re.search(r"block=(\d+)", plan).group(1))
-        fam = fam_of[plan.split("<")[0]]
-        f, w = fetch.get((fam, grid)), write.get((fam, grid))
+        key = (plan_key(plan), grid)
+        f, w = fetch.get(key), write.get(key)
         if not f or not w:
             continue
         fetch_b = 2 * statistics.median(f) * 1024

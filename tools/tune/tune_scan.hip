@@ -223,6 +223,10 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   vs.push_back({"hillis tile U1", true, [=](hipStream_t s) {
                   return launch_tile_scan<float, double, 1, 4, 1, true, 0, false>(x, y, nullptr, n, k, s);
                 }});
+  TILEM(1, 1)
+  TILEM(1, 64)
+  TILEM(4, 1)
+  TILEM(4, 64)
   TILEM(2, 1)
   TILEM(2, 4)
   TILEM(2, 16)
