@@ -223,35 +223,38 @@ def run_workload(args, name, rank, world, with_cpu):
         algo = args.algo
     seed = 0x5EED
     dtype = torch.float32 if dt == "f32" else torch.int16
+    elem = 4 if dt == "f32" else 2
+    # A footprint the 256 MB MALL could partly hold across steps (config #2:
+    # 512 MiB) is timed cold: the step cycles through R copies of (x, y) so
+    # that >= 2 GiB of other traffic separates two uses of the same buffers
+    # (SURVEY.md 8d asks for the MALL to be flushed between iterations).
+    rot = max(1, -(-8 * MALL_BYTES // (2 * elem * n))) if world == 1 else 1
     # weak scaling: this rank holds global samples [rank*n, (rank+1)*n)
-    x = dsp.fill_synthetic(n, dtype, seed=seed, offset=rank * n, device="cuda")
-    y = torch.empty_like(x)
+    xs = [dsp.fill_synthetic(n, dtype, seed=seed, offset=rank * n, device="cuda") for _ in range(rot)]
+    ys = [torch.empty_like(xs[0]) for _ in range(rot)]
+    x, y = xs[0], ys[0]
     hist_buf = torch.empty(max((k - 1) * C, 1), dtype=dtype, device="cuda")
     resolved = dsp.resolve_algo(n, k, C, dsp.F32 if dt == "f32" else dsp.I16, algo)
     launch_plan = dsp.plan(n, k, C, dsp.F32 if dt == "f32" else dsp.I16, algo)
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
-    elem = 4 if dt == "f32" else 2
-    # A footprint the 256 MB MALL can hold a large part of (config #2: 512 MiB)
-    # is also timed cold: a 2x-MALL write between launches evicts it, and that
-    # number is taken from the per-launch events.
-    cold = world == 1 and 2 * elem * n <= 4 * MALL_BYTES
 
-    def step(i=None):
+    def step(i=None, j=0):
         if world > 1:
             # halo send/recv posted first, interior launch overlaps it, head launch after it
             sharded_moving_average(x, k, C, algo, out=y, recv_buf=hist_buf[: (k - 1) * C],
                                    events=ev[i] if i is not None else None)
             return
         if i is not None:
+            j = i % rot
             ev[i][0].record()
-        dsp.moving_average_into(x, y, k, C, algo)
+        dsp.moving_average_into(xs[j], ys[j], k, C, algo)
         if i is not None:
             ev[i][1].record()
 
-    for _ in range(args.warmup):
-        step()
+    for w in range(args.warmup):
+        step(j=w % rot)
     barrier(world)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -262,21 +265,6 @@ def run_workload(args, name, rank, world, with_cpu):
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     kern_avg_ms = statistics.mean(kern_ms)
     kern_avg_ms = max_over_ranks(kern_avg_ms, world)
-    warm = None
-    if cold:
-        flush = torch.empty(2 * MALL_BYTES // 4, dtype=torch.float32, device="cuda")
-        for i in range(args.steps):
-            flush.fill_(float(i))
-            step(i)
-        torch.cuda.synchronize()
-        cold_ms = [a.elapsed_time(b) for a, b in ev]
-        del flush
-        warm = {"value": round(n * args.steps / dt_s / 1e9, 3), "kernel_avg_ms": round(kern_avg_ms, 4),
-                "timing": "back-to-back launches, wall clock"}
-        kern_ms = cold_ms
-        kern_avg_ms = statistics.mean(kern_ms)
-        dt_s = sum(kern_ms) * 1e-3
-
     alg_bytes = 2 * elem * n  # read x once, write y once
     if world > 1:  # events bracket the interior launch only (frames >= head_frames)
         from digital_signal_processsing_amd.shard import head_frames
@@ -309,8 +297,9 @@ def run_workload(args, name, rank, world, with_cpu):
             "parallelism": f"shard{world} (contiguous shards, (k-1)-sample RCCL halo)" if world > 1 else "single GPU",
         },
         "hbm_gbs_algorithmic": round(alg_bytes * world * args.steps / dt_s / 1e9, 1),
-        "timing": ("HIP events per launch, MALL flushed (2x 256 MB write) between launches" if cold
-                   else "wall clock over the timed steps (barrier + synchronize on both sides)"),
+        "timing": "wall clock over the timed steps (barrier + synchronize on both sides)"
+                  + (f"; steps rotate over {rot} input/output buffer pairs so no step finds its data in the "
+                     f"256 MB MALL" if rot > 1 else ""),
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -324,8 +313,6 @@ def run_workload(args, name, rank, world, with_cpu):
             "algorithmic_bytes_per_launch": alg_bytes,
         },
     }
-    if warm is not None:
-        line["warm"] = warm
     if args.check:
         res = check_output(y, n, k, C, dt, seed, rank)
         if world > 1:
@@ -337,7 +324,7 @@ def run_workload(args, name, rank, world, with_cpu):
         line["check"] = res
     if with_cpu and rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"], line["cpu_baseline_multicore"] = cpu_baseline(args, n, k, C, seed)
-    del x, y
+    del x, y, xs, ys
     torch.cuda.empty_cache()
     return line
 
