@@ -85,8 +85,13 @@ def plan(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto") -
 
 
 def moving_average_into(x, out, grade: int, channels: int = 1, algo="auto", history=None,
-                        block_size: int = 0, stream=None) -> None:
-    """Enqueue ``out = moving_average(x)`` on ``stream`` (default: current)."""
+                        block_size: int = 0, stream=None, workspace=None) -> None:
+    """Enqueue ``out = moving_average(x)`` on ``stream`` (default: current).
+
+    ``workspace``: optional caller-owned device buffer (any dtype, contiguous)
+    of at least ``workspace_bytes(...)`` bytes, like the reference's
+    ``DspWorkspace`` scratch; without it the look-back scan (long windows)
+    takes one from torch's caching allocator per call."""
     torch = _torch()
     if not (x.is_cuda and out.is_cuda):
         raise ValueError("x and out must be device tensors (libmavg has no CPU path)")
@@ -102,8 +107,26 @@ def moving_average_into(x, out, grade: int, channels: int = 1, algo="auto", hist
         if history.numel() != (grade - 1) * channels:
             raise ValueError(f"history must hold (grade-1)*channels = {(grade - 1) * channels} samples")
         hist_ptr = history.data_ptr() if history.numel() else None
+    # workspace (look-back scan only): from torch's caching allocator, tied to
+    # the launch stream so it is not handed out again before the kernel ends
     ws_n = workspace_bytes(x.numel(), grade, channels, dt, algo)
-    ws = torch.empty(ws_n, dtype=torch.uint8, device=x.device) if ws_n else None
+    ws = None
+    if ws_n and workspace is not None:
+        if not (workspace.is_cuda and workspace.is_contiguous()):
+            raise ValueError("workspace must be a contiguous device tensor")
+        if workspace.numel() * workspace.element_size() < ws_n:
+            raise ValueError(f"workspace holds {workspace.numel() * workspace.element_size()} bytes, "
+                             f"the launch needs {ws_n}")
+        ws, ws_n = workspace, workspace.numel() * workspace.element_size()
+    elif ws_n:
+        if torch.cuda.is_current_stream_capturing():
+            # a workspace taken from the capture's private pool is freed again
+            # before the capture ends; pass one that outlives the graph
+            raise ValueError(f"grade={grade} uses the look-back scan, which needs a {ws_n}-byte workspace: "
+                             "inside a graph capture pass workspace= (see workspace_bytes())")
+        ws = torch.empty(ws_n, dtype=torch.uint8, device=x.device)
+        if stream is not None and stream != torch.cuda.current_stream(x.device):
+            ws.record_stream(stream)
     st = _lib.load().mavg_run(x.data_ptr(), out.data_ptr(), x.numel(), channels, grade, dt,
                               _algo_code(algo), block_size, hist_ptr,
                               ws.data_ptr() if ws is not None else None, ws_n,

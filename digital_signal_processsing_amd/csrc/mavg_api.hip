@@ -99,15 +99,24 @@ int mavg_workspace_bytes(size_t n_samples, int channels, int grade, int dtype, i
   if (out_bytes == nullptr) return MAVG_ERR_INVALID_ARG;
   const int st = validate(n_samples, channels, grade, dtype, algo);
   if (st != MAVG_OK) return st;
-  *out_bytes = 0;  // every algorithm works from LDS and registers only
+  *out_bytes = 0;
+  if (n_samples == 0) return MAVG_OK;
+  // the dispatch decides; ask it in plan mode (nothing is launched)
+  LaunchPlan plan{};
+  plan.ws_bytes = 0;
+  g_plan = &plan;
+  const int rs = mavg_run(reinterpret_cast<const void*>(uintptr_t(1) << 20), reinterpret_cast<void*>(uintptr_t(1) << 21),
+                          n_samples, channels, grade, dtype, algo, block_size, nullptr, nullptr, 0, nullptr);
+  g_plan = nullptr;
+  if (rs != MAVG_OK) return rs;
+  *out_bytes = plan.ws_bytes;
   return MAVG_OK;
 }
 
 int mavg_run(const void* d_in, void* d_out, size_t n_samples, int channels, int grade, int dtype, int algo,
              int block_size, const void* d_history, void* d_ws, size_t ws_bytes, void* stream) {
-  (void)d_ws;
-  (void)ws_bytes;
   (void)block_size;
+  const Workspace ws{d_ws, ws_bytes};
   int st = validate(n_samples, channels, grade, dtype, algo);
   if (st != MAVG_OK) return st;
   if (n_samples == 0) return MAVG_OK;
@@ -134,9 +143,9 @@ int mavg_run(const void* d_in, void* d_out, size_t n_samples, int channels, int 
     case MAVG_ALGO_HILLIS_SCALAR: {
       const bool vec = (algo == MAVG_ALGO_BLELLOCH || algo == MAVG_ALGO_HILLIS);
       const bool hs = (algo == MAVG_ALGO_HILLIS || algo == MAVG_ALGO_HILLIS_SCALAR);
-      if (f32) return scan_f32(C, vec, hs, d_in, d_out, d_history, nframes, k, s);
-      if (i64acc) return scan_i16_wide(C, vec, hs, d_in, d_out, d_history, nframes, k, s);
-      return scan_i16(C, vec, hs, d_in, d_out, d_history, nframes, k, s);
+      if (f32) return scan_f32(C, vec, hs, d_in, d_out, d_history, nframes, k, s, ws);
+      if (i64acc) return scan_i16_wide(C, vec, hs, d_in, d_out, d_history, nframes, k, s, ws);
+      return scan_i16(C, vec, hs, d_in, d_out, d_history, nframes, k, s, ws);
     }
     case MAVG_ALGO_DIRECT:
     case MAVG_ALGO_DIRECT_VEC2:

@@ -26,6 +26,7 @@ OutParams make_out_params(int k);
 // launchers describe the launch they would make instead of making it.
 struct LaunchPlan {
   char text[160];
+  size_t ws_bytes;  // device workspace the launch needs (mavg_workspace_bytes)
 };
 extern thread_local LaunchPlan* g_plan;
 
@@ -37,12 +38,19 @@ template <> constexpr const char* type_name<int32_t>() { return "i32"; }
 template <> constexpr const char* type_name<int64_t>() { return "i64"; }
 
 // family entry points (defined in mavg_scan_*.hip / mavg_direct.hip)
+// Workspace: the look-back scan needs kLookbackHeader + ntiles*C*8 bytes of
+// caller-owned device memory (reset on the stream before each launch); every
+// other launch needs none.
+struct Workspace {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
 int scan_f32(int C, bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes, int k,
-             hipStream_t st);
+             hipStream_t st, Workspace ws);
 int scan_i16(int C, bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes, int k,
-             hipStream_t st);
+             hipStream_t st, Workspace ws);
 int scan_i16_wide(int C, bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes,
-                  int k, hipStream_t st);
+                  int k, hipStream_t st, Workspace ws);
 int direct_any(int dtype, bool wide, int C, int width, const void* in, void* out, const void* hist,
                long long nframes, int k, hipStream_t st);
 int naive_any(int dtype, bool wide, const void* in, void* out, const void* hist, long long nframes, int C, int k,
@@ -140,39 +148,55 @@ int launch_tile_scan(const void* in, void* out, const void* hist, long long nfra
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
-// Algorithm selection for the scan family (measured on MI355X with
-// tools/tune/tune_scan.hip, see DESIGN.md "Tuning"):
-//   * flat-tile scan with an LDS-staged halo whenever the halo fits: tile of
-//     2 units per lane (8 KiB of samples) for k*C*elem <= 8 KiB, 8 units per
-//     lane (32 KiB) for larger windows;
-//   * segment-streaming scan (LDS ring, pre-roll) when the halo does not fit
-//     the 64 KiB LDS budget; x[n-k] from global memory when even the ring
-//     does not fit.
-template <typename T, typename A, int C, int F, bool HS>
-int dispatch_scan_f(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st) {
+// look-back tile scan (two launches): pass 1 writes every whole tile's sum
+// into the workspace, pass 2 scans each tile with its carry from those sums
+template <typename T, typename A, int C, int F, int U, int NT = 0>
+int launch_lookback_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
+                         Workspace ws, int xcd_remap = kRemapGroup) {
+  constexpr int TF = kWG * F * U;
   constexpr int VE = F * C;
-  constexpr int kUnitBytes = VE * (int)sizeof(T);
-  const long long halo_bytes = (long long)k * C * (long long)sizeof(T);
-  auto tile_lds = [&](int U) -> long long {
-    const long long hu = (k + F - 1) / F;
-    return (hu + (long long)U * kWG + 1) * kUnitBytes + (U * kNW + kNW) * C * (long long)sizeof(A);
-  };
-  if constexpr (sizeof(T) == 2) {
-    // int16: 16 KiB tiles, non-temporal streaming for small halos
-    // (tools/tune/tune_scan.hip ... i16, back-to-back bursts)
-    if (halo_bytes <= 2 * 1024 && tile_lds(4) <= (long long)kLdsBudget)
-      return launch_tile_scan<T, A, C, F, 4, HS, kNtLoad | kNtStore>(in, out, hist, nframes, k, st, kRemapGroup);
-    if (halo_bytes <= 8 * 1024 && tile_lds(4) <= (long long)kLdsBudget)
-      return launch_tile_scan<T, A, C, F, 4, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
-  } else {
-    if (halo_bytes <= 8 * 1024 && tile_lds(2) <= (long long)kLdsBudget)
-      return launch_tile_scan<T, A, C, F, 2, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+  constexpr int NSEG = U * kNW;
+  constexpr size_t kStageBytes = (((size_t)(U * kWG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15;
+  const long long ntiles = (nframes + TF - 1) / TF;
+  const long long nfull = nframes / TF;
+  if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  const size_t need = (size_t)kLookbackHeader + (size_t)std::max<long long>(nfull, 1) * C * sizeof(A);
+  const size_t lds = kStageBytes + (size_t)(NSEG + kNW) * C * sizeof(A);
+  if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text),
+             "lookback_scan<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d> grid=%lld+%lld block=%d lds=%zu tile_frames=%d "
+             "remap=%d ws=%zu",
+             type_name<T>(), type_name<A>(), C, F, U, NT, nfull, ntiles, kWG, lds, TF, xcd_remap, need);
+    g_plan->ws_bytes = need;
+    return MAVG_OK;
   }
-  if (tile_lds(8) <= (long long)kLdsBudget)
-    return launch_tile_scan<T, A, C, F, 8, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
-  // segment streaming: short XCD-remapped segments of at least 4 chunks and
-  // 4x the pre-roll (measured 5.5-5.7 TB/s vs 5.0 for one long segment per
-  // workgroup, tools/tune/tune_scan.hip)
+  if (ws.ptr == nullptr || ws.bytes < need) return MAVG_ERR_WORKSPACE;
+  if ((reinterpret_cast<uintptr_t>(ws.ptr) & 7u) != 0) return MAVG_ERR_MISALIGNED;
+  A* sums = reinterpret_cast<A*>(static_cast<unsigned char*>(ws.ptr) + kLookbackHeader);
+  if (nfull > 0)
+    hipLaunchKernelGGL((tile_sums_kernel<T, A, C, F, U>), dim3((unsigned)nfull), dim3(kWG), 0, st,
+                       static_cast<const T*>(in), sums, nfull, xcd_remap);
+  LookbackParams p{};
+  p.in = in;
+  p.out = out;
+  p.hist = hist;
+  p.nframes = nframes;
+  p.k = k;
+  p.o = make_out_params(k);
+  p.halo_units = (k + F - 1) / F;
+  p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
+  p.xcd_remap = xcd_remap;
+  p.sums = sums;
+  hipLaunchKernelGGL((lookback_scan_kernel<T, A, C, F, U, NT>), dim3((unsigned)ntiles), dim3(kWG), lds, st, p);
+  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+}
+
+// segment streaming with the launch geometry measured best: short
+// XCD-remapped segments of at least 4 chunks and 4x the pre-roll (5.5-5.7
+// TB/s vs 5.0 for one long segment per workgroup, tools/tune/tune_scan.hip)
+template <typename T, typename A, int C, int F, bool HS>
+int launch_segment_rule(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st) {
   constexpr int SU = F >= 4 ? 2 : 8;
   constexpr int CHF = kWG * F * SU;
   ScanTuning t;
@@ -180,33 +204,101 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
   t.seg_chunks = std::max(4, 4 * ((k - 1 + CHF - 1) / CHF));
   return launch_scan<T, A, C, F, SU, HS, 2, 0>(in, out, hist, nframes, k, st, t);
 }
+// ... and whether its LDS ring holds the window (else it re-reads x[n-k]
+// from global memory, measured 0.25-0.40 of peak)
+template <typename T, typename A, int C, int F>
+bool segment_ring_fits(int k) {
+  constexpr int SU = F >= 4 ? 2 : 8;
+  constexpr long long CHF = (long long)kWG * F * SU;
+  const long long ring = ((CHF * (((long long)k + 3 * CHF - 1) / CHF) * C * (long long)sizeof(T)) + 15) & ~15LL;
+  return ring + 2LL * SU * kNW * C * (long long)sizeof(A) <= (long long)kLdsBudget;
+}
+
+// Algorithm selection for the scan family (measured on MI355X with
+// tools/tune/tune_scan.hip + tools/tune/sweep_*.sh, 2^30 samples, back-to-back
+// launches; DESIGN.md "Tuning").  Tiles are 4 KiB of samples per U.
+//   Blelloch flavour, by halo bytes H = k*C*elem:
+//     int16  H <= 256: U2 nt | H <= 4 KiB: U4 nt | H <= 8 KiB: U4 |
+//            mono H <= 16 KiB: U8
+//     fp32   mono H <= 512: U4 nt | H <= 4 KiB: U2 | H <= 16 KiB: U8
+//     longer windows: the segment-streaming scan while its LDS ring holds
+//     the window, then the two-pass look-back scan (needs the workspace)
+//   Hillis-Steele flavour: the halo-staged tile while it fits LDS, then the
+//   segment-streaming scan.
+template <typename T, typename A, int C, int F, bool HS>
+int dispatch_scan_f(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
+                    Workspace ws) {
+  constexpr int VE = F * C;
+  constexpr int kUnitBytes = VE * (int)sizeof(T);
+  const long long halo_bytes = (long long)k * C * (long long)sizeof(T);
+  auto tile_lds = [&](int U) -> long long {
+    const long long hu = (k + F - 1) / F;
+    return (hu + (long long)U * kWG + 1) * kUnitBytes + (U * kNW + kNW) * C * (long long)sizeof(A);
+  };
+  constexpr long long kB = (long long)kLdsBudget;
+  constexpr int kNt = kNtLoad | kNtStore;
+  if constexpr (!HS) {
+    if constexpr (sizeof(T) == 2) {
+      if (halo_bytes <= 256 && tile_lds(2) <= kB)
+        return launch_tile_scan<T, A, C, F, 2, false, kNt>(in, out, hist, nframes, k, st, kRemapGroup);
+      if (halo_bytes <= 4096 && tile_lds(4) <= kB)
+        return launch_tile_scan<T, A, C, F, 4, false, kNt>(in, out, hist, nframes, k, st, kRemapGroup);
+      if (halo_bytes <= 8192 && tile_lds(4) <= kB)
+        return launch_tile_scan<T, A, C, F, 4, false, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+      if (C == 1 && halo_bytes <= 16384 && tile_lds(8) <= kB)
+        return launch_tile_scan<T, A, C, F, 8, false, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+    } else {
+      if (C == 1 && halo_bytes <= 512 && tile_lds(4) <= kB)
+        return launch_tile_scan<T, A, C, F, 4, false, kNt>(in, out, hist, nframes, k, st, kRemapGroup);
+      if (halo_bytes <= 4096 && tile_lds(2) <= kB)
+        return launch_tile_scan<T, A, C, F, 2, false, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+      if (halo_bytes <= 16384 && tile_lds(8) <= kB)
+        return launch_tile_scan<T, A, C, F, 8, false, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+    }
+    if (segment_ring_fits<T, A, C, F>(k)) return launch_segment_rule<T, A, C, F, false>(in, out, hist, nframes, k, st);
+    return launch_lookback_scan<T, A, C, F, 2, 0>(in, out, hist, nframes, k, st, ws);
+  } else {
+    if constexpr (sizeof(T) == 2) {
+      if (halo_bytes <= 2 * 1024 && tile_lds(4) <= kB)
+        return launch_tile_scan<T, A, C, F, 4, HS, kNt>(in, out, hist, nframes, k, st, kRemapGroup);
+      if (halo_bytes <= 8 * 1024 && tile_lds(4) <= kB)
+        return launch_tile_scan<T, A, C, F, 4, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+    } else {
+      if (halo_bytes <= 8 * 1024 && tile_lds(2) <= kB)
+        return launch_tile_scan<T, A, C, F, 2, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+    }
+    if (tile_lds(8) <= kB)
+      return launch_tile_scan<T, A, C, F, 8, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+    return launch_segment_rule<T, A, C, F, HS>(in, out, hist, nframes, k, st);
+  }
+}
 
 template <typename T, typename A, int C>
 int dispatch_scan_c(bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes, int k,
-                    hipStream_t st) {
+                    hipStream_t st, Workspace ws) {
   constexpr int VF = (C * (int)sizeof(T) <= 16 && 16 % (C * (int)sizeof(T)) == 0) ? 16 / (C * (int)sizeof(T)) : 0;
   if constexpr (VF > 0) {
     if (vec) {
-      return hs ? dispatch_scan_f<T, A, C, VF, true>(in, out, hist, nframes, k, st)
-                : dispatch_scan_f<T, A, C, VF, false>(in, out, hist, nframes, k, st);
+      return hs ? dispatch_scan_f<T, A, C, VF, true>(in, out, hist, nframes, k, st, ws)
+                : dispatch_scan_f<T, A, C, VF, false>(in, out, hist, nframes, k, st, ws);
     }
   }
-  return hs ? dispatch_scan_f<T, A, C, 1, true>(in, out, hist, nframes, k, st)
-            : dispatch_scan_f<T, A, C, 1, false>(in, out, hist, nframes, k, st);
+  return hs ? dispatch_scan_f<T, A, C, 1, true>(in, out, hist, nframes, k, st, ws)
+            : dispatch_scan_f<T, A, C, 1, false>(in, out, hist, nframes, k, st, ws);
 }
 
 template <typename T, typename A>
 int dispatch_scan(int C, bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes,
-                  int k, hipStream_t st) {
+                  int k, hipStream_t st, Workspace ws) {
   switch (C) {
-    case 1: return dispatch_scan_c<T, A, 1>(vec, hs, in, out, hist, nframes, k, st);
-    case 2: return dispatch_scan_c<T, A, 2>(vec, hs, in, out, hist, nframes, k, st);
-    case 3: return dispatch_scan_c<T, A, 3>(vec, hs, in, out, hist, nframes, k, st);
-    case 4: return dispatch_scan_c<T, A, 4>(vec, hs, in, out, hist, nframes, k, st);
-    case 5: return dispatch_scan_c<T, A, 5>(vec, hs, in, out, hist, nframes, k, st);
-    case 6: return dispatch_scan_c<T, A, 6>(vec, hs, in, out, hist, nframes, k, st);
-    case 7: return dispatch_scan_c<T, A, 7>(vec, hs, in, out, hist, nframes, k, st);
-    case 8: return dispatch_scan_c<T, A, 8>(vec, hs, in, out, hist, nframes, k, st);
+    case 1: return dispatch_scan_c<T, A, 1>(vec, hs, in, out, hist, nframes, k, st, ws);
+    case 2: return dispatch_scan_c<T, A, 2>(vec, hs, in, out, hist, nframes, k, st, ws);
+    case 3: return dispatch_scan_c<T, A, 3>(vec, hs, in, out, hist, nframes, k, st, ws);
+    case 4: return dispatch_scan_c<T, A, 4>(vec, hs, in, out, hist, nframes, k, st, ws);
+    case 5: return dispatch_scan_c<T, A, 5>(vec, hs, in, out, hist, nframes, k, st, ws);
+    case 6: return dispatch_scan_c<T, A, 6>(vec, hs, in, out, hist, nframes, k, st, ws);
+    case 7: return dispatch_scan_c<T, A, 7>(vec, hs, in, out, hist, nframes, k, st, ws);
+    case 8: return dispatch_scan_c<T, A, 8>(vec, hs, in, out, hist, nframes, k, st, ws);
     default: return MAVG_ERR_UNSUPPORTED;
   }
 }

@@ -6,5 +6,5 @@
 
 namespace mavg {
 template int dispatch_scan_c<MAVG_T, MAVG_A, MAVG_C>(bool, bool, const void*, void*, const void*, long long, int,
-                                                     hipStream_t);
+                                                     hipStream_t, Workspace);
 }  // namespace mavg

@@ -76,7 +76,12 @@ typedef enum {
     MAVG_ERR_HIP = 5          /* a HIP runtime call or kernel launch failed */
 } mavg_status;
 
-/* Device workspace (bytes) mavg_run needs for this problem; 0 is valid. */
+/* Device workspace (bytes) mavg_run needs for this problem.  0 for every
+ * launch except the two-pass look-back scan that AUTO/BLELLOCH pick for
+ * windows too long for LDS (e.g. fp32 k > ~12K frames): 256 + one
+ * accumulator-sized sum per whole tile and channel (4 MiB for 2^30 fp32
+ * samples).  Any alignment of 8 B; contents need no initialisation; one
+ * workspace must not serve two launches that may run concurrently. */
 int mavg_workspace_bytes(size_t n_samples, int channels, int grade, int dtype,
                          int algo, int block_size, size_t* out_bytes);
 

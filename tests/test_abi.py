@@ -89,14 +89,42 @@ def test_plan_describes_launch_without_gpu():
     p = dsp.plan(1 << 30, 1024)
     assert p.startswith("tile_scan<f32,acc=f64,C=1,F=4,U=2,blelloch") and "grid=524288" in p, p
     assert "U=8" in dsp.plan(1 << 30, 4096)
-    assert dsp.plan(1 << 20, 70_000).startswith("segment_scan<") and "xkg=1" in dsp.plan(1 << 20, 70_000)
+    assert dsp.plan(1 << 20, 70_000).startswith("lookback_scan<f32")
+    assert dsp.plan(1 << 20, 70_000, algo="hillis").startswith("segment_scan<") and "xkg=1" in dsp.plan(
+        1 << 20, 70_000, algo="hillis")
     assert dsp.plan(1 << 20, 7, algo="direct").startswith("direct<f32")
     assert dsp.plan(1 << 20, 7, algo="naive").startswith("naive<f32")
     assert "hillis" in dsp.plan(1 << 20, 7, algo="hillis_scalar")
-    assert dsp.plan(1 << 20, 100_000, dtype=dsp.I16).startswith("segment_scan<i16,acc=i64")
+    assert dsp.plan(1 << 20, 100_000, dtype=dsp.I16).startswith("lookback_scan<i16,acc=i64")
     assert dsp.plan(3 * 1000, 7, channels=3, dtype=dsp.I16, algo="blelloch").startswith("tile_scan<i16,acc=i32,C=3,F=1")
     with pytest.raises(dsp.MavgError):
         dsp.plan(10, 0)
+
+
+def test_workspace_only_for_lookback():
+    import digital_signal_processsing_amd as dsp
+    # halo-staged tiles need none; the look-back scan needs a ticket word and
+    # one 8-byte sum per (tile, channel)
+    assert dsp.workspace_bytes(1 << 30, 1024) == 0
+    assert dsp.workspace_bytes(1 << 30, 4096) == 0
+    # k=8192 fp32 still fits the segment scan's LDS ring; k=20000 does not
+    assert dsp.workspace_bytes(1 << 30, 8192) == 0 and dsp.plan(1 << 30, 8192).startswith("segment_scan<")
+    tiles = (1 << 30) // 2048  # whole tiles: one fp64 sum each
+    assert dsp.workspace_bytes(1 << 30, 20_000) == 256 + tiles * 8
+    assert "ws=%d" % (256 + tiles * 8) in dsp.plan(1 << 30, 20_000)
+    n = 2 * 1_000_003
+    st = (n // 2) // 2048     # int16 stereo: one int32 sum per (whole tile, channel)
+    assert dsp.workspace_bytes(n, 44100, 2, dsp.I16) == 256 + st * 2 * 4
+    assert dsp.workspace_bytes(1 << 20, 70_000, algo="hillis") == 0
+    assert dsp.workspace_bytes(0, 70_000) == 0
+
+
+def test_lookback_without_workspace_is_an_error():
+    lib = _lib.load()
+    # plan mode is not used here: a real call with dummy aligned pointers must
+    # refuse before touching the device when the workspace is missing
+    st = lib.mavg_run(1 << 20, 1 << 21, 1 << 20, 1, 70_000, _lib.F32, _lib.ALGO_BLELLOCH, 0, None, None, 0, None)
+    assert st == _lib.ERR_WORKSPACE
 
 
 def test_auto_picks_direct_for_tiny_windows():

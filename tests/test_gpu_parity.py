@@ -192,7 +192,7 @@ def test_checksum_of_checksums_repeatability(gpu):
 
 
 @pytest.mark.parametrize("C,k,dtype", [(1, 1024, "f32"), (2, 41, "i16"), (1, 1, "f32"), (1, 4096, "f32"),
-                                       (2, 70, "f32")])
+                                       (2, 70, "f32"), (1, 9000, "f32"), (1, 30_000, "f32"), (2, 20_000, "i16")])
 def test_sharded_split_launch_equals_whole_signal(oracle_mod, gpu, C, k, dtype):
     """The multi-GPU step on one GPU: every shard filtered as interior launch +
     head launch with the previous shard's tail as history (what rank r does
@@ -278,3 +278,123 @@ def test_many_channels_auto(oracle_mod, gpu):
         else:
             x = oracle_mod.synth_f32(3001 * C, offset=C, dist=1)
             assert_f32_close(_run(x, 37, C, "auto", gpu), oracle_mod.mavg_f32(x, 37, C), "C=16")
+
+
+# ---------------------------------------------------------------------------
+# look-back tile scan (long windows): carry from the pass-1 tile sums
+def _lookback_tile(dsp, n, k, C, dt):
+    plan = dsp.plan(n, k, C, dt)
+    assert plan.startswith("lookback_scan<"), plan
+    return int(plan.split("tile_frames=")[1].split()[0])
+
+
+@pytest.mark.parametrize("C", [1, 2, 3, 8])
+@pytest.mark.parametrize("dtype", ["i16", "f32"])
+def test_lookback_window_edges(oracle_mod, gpu, C, dtype):
+    """k just below / at / above multiples of the tile (empty, one-frame and
+    full partial pieces), windows spanning many tiles, int16 k > 65535, and a
+    ragged tail tile."""
+    import digital_signal_processsing_amd as dsp
+    dt = dsp.F32 if dtype == "f32" else dsp.I16
+    frames = 200_003
+    T = _lookback_tile(dsp, frames * C, 70_001, C, dt)
+    for k in sorted({16 * T - 1, 16 * T, 16 * T + 1, 20_000, 44_100, 70_001}):
+        if dsp.plan(frames * C, k, C, dt).split("<")[0] != "lookback_scan":
+            continue
+        if dtype == "i16":
+            x = oracle_mod.synth_i16(frames * C, offset=k + C)
+            assert np.array_equal(_run(x, k, C, "blelloch", gpu), oracle_mod.mavg_i16(x, k, C)), (C, k)
+        else:
+            x = oracle_mod.synth_f32(frames * C, offset=k + C, dist=1)
+            assert_f32_close(_run(x, k, C, "blelloch", gpu), oracle_mod.mavg_f32(x, k, C), f"C={C} k={k}")
+
+
+@pytest.mark.parametrize("frames", [1, 777, 44_099, 44_100, 44_101, 100_000])
+def test_lookback_short_signals(oracle_mod, gpu, frames):
+    """Signals shorter than (or about as long as) the window: every tile's
+    window reaches before frame 0."""
+    k, C = 44_100, 2
+    x = oracle_mod.synth_i16(frames * C, offset=frames)
+    assert np.array_equal(_run(x, k, C, "auto", gpu), oracle_mod.mavg_i16(x, k, C))
+    xf = oracle_mod.synth_f32(frames * C, offset=frames, dist=1)
+    assert_f32_close(_run(xf, k, C, "auto", gpu), oracle_mod.mavg_f32(xf, k, C), f"frames={frames}")
+
+
+@pytest.mark.parametrize("dtype", ["i16", "f32"])
+@pytest.mark.parametrize("cut", [5_000, 37_001])
+def test_lookback_history_equals_concatenation(oracle_mod, gpu, dtype, cut):
+    """History with a long window: the part of the window before frame 0 comes
+    from the history buffer (cut < k: the window also reaches before it)."""
+    C, k, frames = 2, 20_000, 120_000
+    if dtype == "i16":
+        x = oracle_mod.synth_i16(frames * C, offset=5)
+        full = oracle_mod.mavg_i16(x, k, C)
+    else:
+        x = oracle_mod.synth_f32(frames * C, offset=5, dist=1)
+        full = oracle_mod.mavg_f32(x, k, C)
+    lo = max(0, cut - (k - 1))
+    hist = np.zeros((k - 1) * C, dtype=x.dtype)
+    hist[(k - 1 - (cut - lo)) * C:] = x[lo * C: cut * C]
+    y = _run(x[cut * C:], k, C, "blelloch", gpu, history=hist)
+    if dtype == "i16":
+        assert np.array_equal(y, full[cut * C:])
+    else:
+        assert_f32_close(y, full[cut * C:], f"cut={cut}")
+
+
+@pytest.mark.parametrize("own_workspace", [True, False])
+def test_lookback_graph_capture(oracle_mod, gpu, own_workspace):
+    """The workspace reset and the look-back launch replay correctly from a
+    captured HIP graph, repeatedly, with a caller-owned workspace; without one
+    the binding refuses inside a capture (no workspace from the capture's
+    private pool, which is freed again before the capture ends)."""
+    import digital_signal_processsing_amd as dsp
+    import torch
+    n, k = 1_000_003, 30_000
+    x = torch.from_numpy(oracle_mod.synth_f32(n, seed=23, dist=1)).to(gpu)
+    y = torch.empty_like(x)
+    assert dsp.plan(n, k).startswith("lookback_scan<")
+    ws = torch.empty(dsp.workspace_bytes(n, k), dtype=torch.uint8, device=gpu) if own_workspace else None
+    s = torch.cuda.Stream(device=gpu)
+    s.wait_stream(torch.cuda.current_stream(gpu))
+    with torch.cuda.stream(s):
+        dsp.moving_average_into(x, y, k, workspace=ws)  # warm-up outside capture
+    torch.cuda.current_stream(gpu).wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    if not own_workspace:
+        # the binding refuses to take a workspace from the capture's pool
+        with pytest.raises(ValueError, match="workspace="):
+            with torch.cuda.graph(g):
+                dsp.moving_average_into(x, y, k)
+        return
+    with torch.cuda.graph(g):
+        dsp.moving_average_into(x, y, k, workspace=ws)
+    ref = oracle_mod.mavg_f32(oracle_mod.synth_f32(n, seed=23, dist=1), k, 1)
+    for i in range(3):
+        y.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert_f32_close(y.cpu().numpy(), ref, f"replay {i}")
+
+
+def test_lookback_large_stereo_slices(oracle_mod, gpu):
+    """2^27 int16 stereo samples, one-second window at 44.1 kHz (k=44100):
+    bit-exact at random slices, the first tiles and the tail."""
+    import digital_signal_processsing_amd as dsp
+    import torch
+    C, k, seed = 2, 44_100, 0x5EED
+    n = 1 << 27
+    x = dsp.fill_synthetic(n, torch.int16, seed=seed, device=gpu)
+    y = dsp.moving_average(x, k, channels=C).cpu().numpy()
+    del x
+    frames = n // C
+    rng = np.random.default_rng(1)
+    span = 3000
+    starts = [0, 2048, 44_000, frames - span] + list(rng.integers(0, frames - span, 40))
+    for s in starts:
+        s = int(s)
+        a = max(0, s - k + 1)
+        xs = oracle_mod.synth_i16((s + span - a) * C, seed=seed, offset=a * C)
+        ref = oracle_mod.mavg_i16(xs, k, C)[(s - a) * C:]
+        assert np.array_equal(y[s * C:(s + span) * C], ref), f"slice at frame {s}"

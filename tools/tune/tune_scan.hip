@@ -3,7 +3,8 @@
 // variants in ONE process, interleaved rounds, median and min reported).
 // Every scan variant's output is compared bit-for-bit with the first one.
 //
-// build: make -C tools/tune      run: tools/tune/tune_scan [log2n] [k] [rounds]
+// build: make -C tools/tune
+// run:   tools/tune/tune_scan [log2n] [k] [rounds] [f32|i16] [burst] [filter] [channels (i16: 1|2)]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -78,6 +79,8 @@ template <typename T, typename A>
 void add_variants(std::vector<struct Variant>& vs, T* x, T* y, long long n, int k);
 
 static int g_burst = 1;  // launches per timed sample (back-to-back, like bench.py's steps)
+static int g_channels = 1;  // 2: int16 stereo variants (interleaved frames)
+static Workspace g_ws;      // look-back scan workspace (64 MiB, allocated in run())
 static std::string g_filter;  // "a|b": keep only variants whose name contains a or b
 
 static bool keep(const std::string& name) {
@@ -102,6 +105,8 @@ int run(int lg, int k, int rounds) {
   CK(hipMalloc(&yref, n * ES));
   unsigned long long* dcnt;
   CK(hipMalloc(&dcnt, 8));
+  g_ws.bytes = 64u << 20;
+  CK(hipMalloc(&g_ws.ptr, g_ws.bytes));
   hipStream_t st;
   CK(hipStreamCreate(&st));
   hipLaunchKernelGGL(synth_kernel<T>, dim3(4096), dim3(256), 0, st, x, n, (uint64_t)0x5EED, 0);
@@ -133,6 +138,15 @@ int run(int lg, int k, int rounds) {
   CK(hipEventCreate(&e1));
   // reference output + correctness of every scan variant
   bool have_ref = false;
+  {  // drop variants the launcher refuses (e.g. LDS over budget for this k)
+    std::vector<Variant> ok;
+    for (auto& v : vs) {
+      if (v.launch(st) != 0) printf("%s: launch refused, skipped\n", v.name.c_str());
+      else ok.push_back(v);
+    }
+    vs.swap(ok);
+    CK(hipStreamSynchronize(st));
+  }
   for (auto& v : vs) {
     if (!v.is_scan) continue;
     if (v.launch(st) != 0) { printf("%s: launch failed\n", v.name.c_str()); return 1; }
@@ -223,6 +237,30 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   vs.push_back({"hillis tile U1", true, [=](hipStream_t s) {
                   return launch_tile_scan<float, double, 1, 4, 1, true, 0, false>(x, y, nullptr, n, k, s);
                 }});
+  // clean grid for the dispatch rules (tools/tune/sweep_shapes.sh)
+#define LB(U)                                                                                           \
+  vs.push_back({"lookback U" #U, true, [=](hipStream_t s) {                                               \
+                  return launch_lookback_scan<float, double, 1, 4, U, 0>(x, y, nullptr, n, k, s, g_ws);        \
+                }});
+  LB(1)
+  LB(2)
+  LB(4)
+  TILE(1, 0, 64)
+  TILE(2, 0, 64)
+  TILE(2, 3, 64)
+  TILE(4, 0, 64)
+  TILE(4, 3, 64)
+  TILE(8, 0, 64)
+  TILE(8, 3, 64)
+  vs.push_back({"seg rule", true, [=](hipStream_t s) {
+                  ScanTuning t;
+                  t.xcd_remap = 1;
+                  t.seg_chunks = std::max(4, 4 * ((k - 1 + 2047) / 2048));
+                  return launch_scan<float, double, 1, 4, 2, false, 2, 0>(x, y, nullptr, n, k, s, t);
+                }});
+  vs.push_back({"f32 product mavg_run", true, [=](hipStream_t s) {
+                  return mavg_run(x, y, n, 1, k, MAVG_F32, MAVG_ALGO_AUTO, 0, nullptr, g_ws.ptr, g_ws.bytes, s);
+                }});
   TILEM(1, 1)
   TILEM(1, 64)
   TILEM(4, 1)
@@ -261,20 +299,60 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                 }});
 #define IPROD()                                                                                           \
   vs.push_back({"i16 product mavg_run", true, [=](hipStream_t s) {                                        \
-                  return mavg_run(x, y, n, 1, k, MAVG_I16, MAVG_ALGO_AUTO, 0, nullptr, nullptr, 0, s);       \
+                  return mavg_run(x, y, n, 1, k, MAVG_I16, MAVG_ALGO_AUTO, 0, nullptr, g_ws.ptr, g_ws.bytes, s); \
                 }});
 #define IDIRECT(U)                                                                                        \
   vs.push_back({"i16 direct U" #U, true, [=](hipStream_t s) {                                              \
                   return launch_direct<int16_t, int32_t, 1, 8, U>(x, y, nullptr, n, k, s, 1);               \
                 }});
-  ITILE(2, 1)
-  ITILE(4, 64)
-  ITILENT(2, 3)
+#define STILE(U, NT, M)                                                                                   \
+  vs.push_back({"i16 stereo tile U" #U " NT" #NT " remap" #M, true, [=](hipStream_t s) {                   \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, false>(x, y, nullptr, n / 2, k, s, M); \
+                }});
+  if (g_channels == 2) {
+    vs.push_back({"i16 stereo product mavg_run", true, [=](hipStream_t s) {
+                    return mavg_run(x, y, n, 2, k, MAVG_I16, MAVG_ALGO_AUTO, 0, nullptr, g_ws.ptr, g_ws.bytes, s);
+                  }});
+#define SLB(U)                                                                                          \
+  vs.push_back({"i16 stereo lookback U" #U, true, [=](hipStream_t s) {                                    \
+                  return launch_lookback_scan<int16_t, int32_t, 2, 4, U, 0>(x, y, nullptr, n / 2, k, s, g_ws); \
+                }});
+    SLB(1)
+    SLB(2)
+    SLB(4)
+    STILE(2, 0, 64)
+    STILE(2, 3, 64)
+    STILE(4, 0, 64)
+    STILE(4, 3, 64)
+    STILE(8, 0, 64)
+    STILE(8, 3, 64)
+    vs.push_back({"i16 stereo seg rule", true, [=](hipStream_t s) {
+                    ScanTuning t;
+                    t.xcd_remap = 1;
+                    t.seg_chunks = std::max(4, 4 * ((k - 1 + 2047) / 2048));
+                    return launch_scan<int16_t, int32_t, 2, 4, 2, false, 2, 0>(x, y, nullptr, n / 2, k, s, t);
+                  }});
+    return;
+  }
+#define ILB(U)                                                                                          \
+  vs.push_back({"i16 lookback U" #U, true, [=](hipStream_t s) {                                           \
+                  return launch_lookback_scan<int16_t, int32_t, 1, 8, U, 0>(x, y, nullptr, n, k, s, g_ws);     \
+                }});
+  ILB(1)
+  ILB(2)
+  ILB(4)
+  ITILENTR(2, 0, 64)
   ITILENTR(2, 3, 64)
-  ITILENTR(2, 3, 16)
-  ITILENTR(2, 3, 256)
+  ITILENTR(4, 0, 64)
   ITILENTR(4, 3, 64)
-  ITILENTR(2, 3, 0)
+  ITILENTR(8, 0, 64)
+  ITILENTR(8, 3, 64)
+  vs.push_back({"i16 seg rule", true, [=](hipStream_t s) {
+                  ScanTuning t;
+                  t.xcd_remap = 1;
+                  t.seg_chunks = std::max(4, 4 * ((k - 1 + 4095) / 4096));
+                  return launch_scan<int16_t, int32_t, 1, 8, 2, false, 2, 0>(x, y, nullptr, n, k, s, t);
+                }});
   IPROD()
   if (k <= 64) {
     IDIRECT(1)
@@ -289,6 +367,7 @@ int main(int argc, char** argv) {
   const std::string dt = argc > 4 ? argv[4] : "f32";
   g_burst = argc > 5 ? atoi(argv[5]) : 1;
   g_filter = argc > 6 ? argv[6] : "";
+  g_channels = argc > 7 ? atoi(argv[7]) : 1;
   printf("burst=%d (launches per timed sample)\n", g_burst);
   return dt == "i16" ? run<int16_t, int32_t>(lg, k, rounds) : run<float, double>(lg, k, rounds);
 }
