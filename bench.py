@@ -310,6 +310,7 @@ def run_workload(args, name, rank, world, with_cpu):
             "kernel": launch_plan,
             "kernel_avg_ms": round(kern_avg_ms, 4),
             "kernel_min_ms": round(min(kern_ms), 4),
+            "kernel_median_ms": round(statistics.median(kern_ms), 4),
             "algorithmic_bytes_per_launch": alg_bytes,
         },
     }

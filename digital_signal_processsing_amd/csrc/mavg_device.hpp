@@ -1,0 +1,228 @@
+// mavg_device.hpp -- device building blocks shared by the kernels (gfx950, wave64):
+// accumulator conversion, DPP wave scans, output conversion, 16-B lane units,
+// guarded element access, the XCD-aware tile mapping.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mavg {
+
+constexpr int kWG = 256;          // threads per workgroup (4 wave64s)
+constexpr int kNW = kWG / 64;     // waves per workgroup
+
+// ----------------------------------------------------------------------------
+// small helpers
+// ----------------------------------------------------------------------------
+template <typename A> __device__ __forceinline__ A to_acc(float x) { return (A)x; }
+template <typename A> __device__ __forceinline__ A to_acc(int16_t x) { return (A)x; }
+
+// 64-lane DPP move with zero fill for invalid / masked lanes.
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int32_t dpp(int32_t v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, BM, false);
+}
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ double dpp(double v) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, BM, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, BM, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int64_t dpp(int64_t v) {
+  int lo = (int)(uint32_t)v, hi = (int)(uint32_t)((uint64_t)v >> 32);
+  lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, BM, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, BM, false);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// Inclusive scan across the 64 lanes of a wave: Kogge-Stone inside each
+// 16-lane row (row_shr 1,2,4,8) then row_bcast:15 / row_bcast:31 to carry
+// row totals across rows -- 6 DPP steps, no LDS.
+template <typename A>
+__device__ __forceinline__ A wave_incl_scan(A v) {
+  v += dpp<0x111, 0xf, 0xf>(v);
+  v += dpp<0x112, 0xf, 0xf>(v);
+  v += dpp<0x114, 0xf, 0xf>(v);
+  v += dpp<0x118, 0xf, 0xf>(v);
+  v += dpp<0x142, 0xa, 0xf>(v);
+  v += dpp<0x143, 0xc, 0xf>(v);
+  return v;
+}
+
+__device__ __forceinline__ int32_t readlane(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ double readlane(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ int64_t readlane(int64_t v, int l) {
+  uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ double shfl_up(double v, int d) { return __shfl_up(v, d, 64); }
+__device__ __forceinline__ int32_t shfl_up(int32_t v, int d) { return __shfl_up(v, d, 64); }
+__device__ __forceinline__ int64_t shfl_up(int64_t v, int d) {
+  return (int64_t)__shfl_up((long long)v, d, 64);
+}
+
+// ----------------------------------------------------------------------------
+// output conversion: window sum -> sample
+// ----------------------------------------------------------------------------
+struct OutParams {
+  double inv_k;     // 1/k (fp32 output, int64 path estimate)
+  uint32_t magic;   // int16/int32 path: q = umulhi(|S|, magic) >> shift
+  int shift;
+  int k;            // divisor
+};
+
+__device__ __forceinline__ float to_out_f32(double s, const OutParams& o) {
+  return (float)(s * o.inv_k);
+}
+// exact C++ truncating division S / k for |S| < 2^31, k <= 65535
+__device__ __forceinline__ int16_t to_out_i16(int32_t s, const OutParams& o) {
+  uint32_t a = s < 0 ? (uint32_t)(-s) : (uint32_t)s;
+  uint32_t q = (o.k == 1) ? a : (__umulhi(a, o.magic) >> o.shift);
+  return (int16_t)(s < 0 ? -(int32_t)q : (int32_t)q);
+}
+// exact truncating division for the int64 path (k > 65535; |S| <= 32768*k).
+// The quotient is at most 2^15, so the fp64 estimate fl(|S| * fl(1/k)) lies
+// within 2^15 * 2^-51.8 = 2^-36.8 of |S|/k, whose fractional part is 0 or at
+// least 1/k > 2^-31: truncation is exact except when k divides |S|, where it
+// may land one below -- fixed by one 32x32->64 multiply-compare, no loops.
+__device__ __forceinline__ int16_t to_out_i16(int64_t s, const OutParams& o) {
+  const uint64_t a = s < 0 ? (uint64_t)(-s) : (uint64_t)s;  // < 2^47
+  const double ad = (double)(uint32_t)(a >> 32) * 4294967296.0 + (double)(uint32_t)a;  // exact
+  uint32_t q = (uint32_t)(ad * o.inv_k);
+  q += a >= (uint64_t)(q + 1u) * (uint64_t)(uint32_t)o.k ? 1u : 0u;
+  return (int16_t)(s < 0 ? -(int32_t)q : (int32_t)q);
+}
+template <typename T, typename A>
+__device__ __forceinline__ T to_out(A s, const OutParams& o);
+template <> __device__ __forceinline__ float to_out<float, double>(double s, const OutParams& o) { return to_out_f32(s, o); }
+template <> __device__ __forceinline__ int16_t to_out<int16_t, int32_t>(int32_t s, const OutParams& o) { return to_out_i16(s, o); }
+template <> __device__ __forceinline__ int16_t to_out<int16_t, int64_t>(int64_t s, const OutParams& o) { return to_out_i16(s, o); }
+
+// ----------------------------------------------------------------------------
+// a "unit" = the F frames x C channels one lane owns per load instruction
+// ----------------------------------------------------------------------------
+template <typename T, int VE>
+struct Unit {
+  T e[VE];
+};
+
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <int BYTES> struct RawVec;
+template <> struct RawVec<32> { using type = u32x8; };
+template <> struct RawVec<16> { using type = u32x4; };
+template <> struct RawVec<8> { using type = u32x2; };
+template <> struct RawVec<4> { using type = uint32_t; };
+template <> struct RawVec<2> { using type = uint16_t; };
+
+template <typename T, int VE>
+struct UnitIO {
+  static constexpr int kBytes = VE * (int)sizeof(T);
+  static constexpr bool kVec = (kBytes == 32 || kBytes == 16 || kBytes == 8 || kBytes == 4 || kBytes == 2);
+
+  // p is aligned to kBytes when kVec (checked on the host for the base pointer).
+  // NT: non-temporal hint (streamed-once HBM data; never used on LDS).
+  template <bool NT = false>
+  __device__ __forceinline__ static Unit<T, VE> load(const T* __restrict__ p) {
+    Unit<T, VE> u;
+    if constexpr (kVec) {
+      using R = typename RawVec<kBytes>::type;
+      R r;
+      if constexpr (NT) r = __builtin_nontemporal_load(reinterpret_cast<const R*>(p));
+      else r = *reinterpret_cast<const R*>(p);
+      __builtin_memcpy(&u, &r, kBytes);
+    } else {
+#pragma unroll
+      for (int i = 0; i < VE; ++i) u.e[i] = p[i];
+    }
+    return u;
+  }
+  template <bool NT = false>
+  __device__ __forceinline__ static void store(T* __restrict__ p, const Unit<T, VE>& u) {
+    if constexpr (kVec) {
+      using R = typename RawVec<kBytes>::type;
+      R r;
+      __builtin_memcpy(&r, &u, kBytes);
+      if constexpr (NT) __builtin_nontemporal_store(r, reinterpret_cast<R*>(p));
+      else *reinterpret_cast<R*>(p) = r;
+    } else {
+#pragma unroll
+      for (int i = 0; i < VE; ++i) p[i] = u.e[i];
+    }
+  }
+};
+
+// extract elements [O, O+VE) of the concatenation (a, b)
+template <int O, typename T, int VE>
+__device__ __forceinline__ Unit<T, VE> extract_at(const Unit<T, VE>& a, const Unit<T, VE>& b) {
+  Unit<T, VE> r;
+#pragma unroll
+  for (int i = 0; i < VE; ++i) r.e[i] = (i + O < VE) ? a.e[i + O] : b.e[i + O - VE];
+  return r;
+}
+template <int O, typename T, int VE>
+__device__ __forceinline__ Unit<T, VE> extract_from(const Unit<T, VE>& a, const Unit<T, VE>& b, int o) {
+  if constexpr (O + 1 >= VE) {
+    return extract_at<O>(a, b);
+  } else {
+    if (o == O) return extract_at<O>(a, b);
+    return extract_from<O + 1>(a, b, o);
+  }
+}
+template <typename T, int VE>
+__device__ __forceinline__ Unit<T, VE> extract(const Unit<T, VE>& a, const Unit<T, VE>& b, int o) {
+  // o is uniform across the grid (depends only on k*C mod VE): a chain of
+  // scalar compares, one static extraction taken
+  return extract_from<0>(a, b, o);
+}
+
+// ----------------------------------------------------------------------------
+// guarded element access: frames < 0 come from the history (the multi-GPU
+// halo / the reference's zero halo, gpu_utils.h:112-123), frames >= nframes
+// and frames before the history read as zero.
+// ----------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T load_elem(const T* __restrict__ in, const T* __restrict__ hist,
+                                       long long f, int c, int C, long long nframes, int k) {
+  if (f >= 0) return f < nframes ? in[f * C + c] : (T)0;
+  if (hist != nullptr && f >= -(long long)(k - 1)) return hist[(f + (k - 1)) * C + c];
+  return (T)0;
+}
+
+// ----------------------------------------------------------------------------
+// tile -> workgroup mapping
+// ----------------------------------------------------------------------------
+// Tile -> workgroup remaps (speed only, never correctness: blocks b and b+8
+// share an XCD under the observed round-robin dispatch, cdna_hip_programming.md
+// 5.5 T1).  32-bit scalar arithmetic only (the grid is < 2^31 workgroups):
+// a 64-bit divide here costs ~150 SALU instructions per wave.
+// mode 0: identity; 1: each XCD takes one contiguous run of nb/8 tiles
+// (bijective for any nb); G = 2^g > 1: each XCD takes runs of G consecutive
+// tiles and the 8 XCDs' runs are adjacent, so the whole chip works inside a
+// window of 8G tiles; blocks past the last full group of 8G map to themselves.
+__device__ __forceinline__ long long remap_tile(unsigned b, unsigned nb, int mode) {
+  if (mode == 0) return b;
+  if (mode == 1) {
+    const unsigned q = nb >> 3, r = nb & 7u, x = b & 7u;
+    return (long long)((x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3));
+  }
+  const unsigned g = (unsigned)__builtin_ctz((unsigned)mode);  // mode = G, a power of two
+  const unsigned full = nb & ~((8u << g) - 1u);
+  if (b >= full) return b;
+  const unsigned i = b >> 3, x = b & 7u;
+  return (long long)(((i >> g) << (g + 3)) + (x << g) + (i & ((1u << g) - 1u)));
+}
+
+// non-temporal (streamed-once) policy bits of the NT template parameters
+constexpr int kNtStore = 1;
+constexpr int kNtLoad = 2;
+
+}  // namespace mavg

@@ -160,7 +160,8 @@ int launch_lookback_scan(const void* in, void* out, const void* hist, long long 
   const long long ntiles = (nframes + TF - 1) / TF;
   const long long nfull = nframes / TF;
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
-  const size_t need = (size_t)kLookbackHeader + (size_t)std::max<long long>(nfull, 1) * C * sizeof(A);
+  using SA = typename ScanAcc<T, A>::type;  // whole-tile sums
+  const size_t need = (size_t)kLookbackHeader + (size_t)std::max<long long>(nfull, 1) * C * sizeof(SA);
   const size_t lds = kStageBytes + (size_t)(NSEG + kNW) * C * sizeof(A);
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
@@ -173,7 +174,7 @@ int launch_lookback_scan(const void* in, void* out, const void* hist, long long 
   }
   if (ws.ptr == nullptr || ws.bytes < need) return MAVG_ERR_WORKSPACE;
   if ((reinterpret_cast<uintptr_t>(ws.ptr) & 7u) != 0) return MAVG_ERR_MISALIGNED;
-  A* sums = reinterpret_cast<A*>(static_cast<unsigned char*>(ws.ptr) + kLookbackHeader);
+  SA* sums = reinterpret_cast<SA*>(static_cast<unsigned char*>(ws.ptr) + kLookbackHeader);
   if (nfull > 0)
     hipLaunchKernelGGL((tile_sums_kernel<T, A, C, F, U>), dim3((unsigned)nfull), dim3(kWG), 0, st,
                        static_cast<const T*>(in), sums, nfull, xcd_remap);

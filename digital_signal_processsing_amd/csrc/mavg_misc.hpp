@@ -1,0 +1,50 @@
+// mavg_misc.hpp -- the naive per-sample kernel and the synthetic-input generator.
+#pragma once
+
+#include "mavg_device.hpp"
+
+namespace mavg {
+
+// ----------------------------------------------------------------------------
+// naive kernel: one thread per sample, k reads from global memory
+// (profilable_parallel_averager.cu:14-23, with the history contract instead
+// of reading before the buffer).
+// ----------------------------------------------------------------------------
+template <typename T, typename A>
+__global__ __launch_bounds__(kWG) void naive_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                    const T* __restrict__ hist, long long nframes,
+                                                    int C, int k, OutParams o) {
+  const long long idx = (long long)blockIdx.x * kWG + threadIdx.x;
+  const long long n = nframes * C;
+  if (idx >= n) return;
+  const long long f = idx / C;
+  const int c = (int)(idx - f * C);
+  A s = (A)0;
+  for (int j = 0; j < k; ++j) s += to_acc<A>(load_elem(in, hist, f - j, c, C, nframes, k));
+  out[idx] = to_out<T, A>(s, o);
+}
+
+// ----------------------------------------------------------------------------
+// synthetic input: identical to oracle/mavg_oracle.c (oracle_synth_*)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kWG) void synth_kernel(T* __restrict__ out, long long n, uint64_t base, int dist) {
+  const long long stride = (long long)gridDim.x * kWG;
+  for (long long i = (long long)blockIdx.x * kWG + threadIdx.x; i < n; i += stride) {
+    const uint64_t h = splitmix64(base + (uint64_t)i);
+    if constexpr (sizeof(T) == 2) {
+      out[i] = (T)(int16_t)(uint16_t)(h >> 48);
+    } else {
+      out[i] = dist == 1 ? (float)(h >> 40) * (1.0f / 16777216.0f) : (float)(int16_t)(uint16_t)(h >> 48);
+    }
+  }
+}
+
+}  // namespace mavg

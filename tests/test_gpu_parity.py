@@ -342,6 +342,20 @@ def test_lookback_history_equals_concatenation(oracle_mod, gpu, dtype, cut):
         assert_f32_close(y, full[cut * C:], f"cut={cut}")
 
 
+def test_int64_division_edges(oracle_mod, gpu):
+    """k > 65535 (int64 window sums): extreme constant signals make k divide
+    the window sum exactly in the steady state and at many warm-up frames --
+    the case the fp64 quotient estimate has to correct."""
+    for k in (65_536, 70_001, 131_072):
+        for c in (-32768, 32767, -1, 12345):
+            x = np.full(300_000, c, dtype=np.int16)
+            y = _run(x, k, 1, "auto", gpu)
+            assert np.array_equal(y, oracle_mod.mavg_i16(x, k, 1)), (k, c)
+            assert (y[k - 1:] == c).all()
+        x = oracle_mod.synth_i16(2 * 250_000, offset=k)
+        assert np.array_equal(_run(x, k, 2, "auto", gpu), oracle_mod.mavg_i16(x, k, 2)), k
+
+
 @pytest.mark.parametrize("own_workspace", [True, False])
 def test_lookback_graph_capture(oracle_mod, gpu, own_workspace):
     """The workspace reset and the look-back launch replay correctly from a

@@ -247,6 +247,8 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   LB(4)
   TILE(1, 0, 64)
   TILE(2, 0, 64)
+  TILE(2, 1, 64)
+  TILE(2, 2, 64)
   TILE(2, 3, 64)
   TILE(4, 0, 64)
   TILE(4, 3, 64)
