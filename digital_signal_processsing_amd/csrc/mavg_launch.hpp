@@ -116,7 +116,7 @@ int launch_scan(const void* in, void* out, const void* hist, long long nframes, 
 
 // flat-tile scan: one workgroup per tile, carry rebuilt from the k-frame halo
 template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, bool GX = false,
-          int WG = kWG>
+          int WG = kWG, bool RC = true>
 int launch_tile_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
                      int xcd_remap = kRemapGroup) {
   constexpr int TF = WG * F * U;
@@ -139,12 +139,14 @@ int launch_tile_scan(const void* in, void* out, const void* hist, long long nfra
   if (p.ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,gx=%d> grid=%lld block=%d lds=%zu tile_frames=%d remap=%d",
-             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)GX, p.ntiles, WG, lds,
-             TF, xcd_remap);
+             "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,gx=%d,rc=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
+             "remap=%d",
+             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)GX, (int)RC,
+             p.ntiles, WG, lds, TF, xcd_remap);
     return MAVG_OK;
   }
-  hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, GX, WG>), dim3((unsigned)p.ntiles), dim3(WG), lds, st, p);
+  hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, GX, WG, RC>), dim3((unsigned)p.ntiles), dim3(WG), lds, st,
+                     p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
@@ -220,8 +222,8 @@ bool segment_ring_fits(int k) {
 // launches; DESIGN.md "Tuning").  Tiles are 4 KiB of samples per U.
 //   Blelloch flavour, by halo bytes H = k*C*elem:
 //     int16  H <= 256: U2 nt | H <= 4 KiB: U4 nt | H <= 8 KiB: U4 |
-//            mono H <= 16 KiB: U8
-//     fp32   mono H <= 512: U4 nt | H <= 4 KiB: U2 | H <= 16 KiB: U8
+//            H <= 16 KiB: U8 (mono) / U4 (multi-channel)
+//     fp32   mono H <= 512: U2 nt rc | H <= 4 KiB: U2 rc | H <= 16 KiB: U8 rc
 //     longer windows: the segment-streaming scan while its LDS ring holds
 //     the window, then the two-pass look-back scan (needs the workspace)
 //   Hillis-Steele flavour: the halo-staged tile while it fits LDS, then the
@@ -239,22 +241,26 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
   constexpr long long kB = (long long)kLdsBudget;
   constexpr int kNt = kNtLoad | kNtStore;
   if constexpr (!HS) {
+    // RC (in-lane prefix rebuilt after the barrier): on for fp32, off for
+    // int16 (measured both ways, tools/tune/ab_rc.sh, sweep_lookback2.sh)
     if constexpr (sizeof(T) == 2) {
       if (halo_bytes <= 256 && tile_lds(2) <= kB)
-        return launch_tile_scan<T, A, C, F, 2, false, kNt>(in, out, hist, nframes, k, st, kRemapGroup);
+        return launch_tile_scan<T, A, C, F, 2, false, kNt, false, kWG, false>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 4096 && tile_lds(4) <= kB)
-        return launch_tile_scan<T, A, C, F, 4, false, kNt>(in, out, hist, nframes, k, st, kRemapGroup);
+        return launch_tile_scan<T, A, C, F, 4, false, kNt, false, kWG, false>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 8192 && tile_lds(4) <= kB)
-        return launch_tile_scan<T, A, C, F, 4, false, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+        return launch_tile_scan<T, A, C, F, 4, false, 0, false, kWG, false>(in, out, hist, nframes, k, st);
       if (C == 1 && halo_bytes <= 16384 && tile_lds(8) <= kB)
-        return launch_tile_scan<T, A, C, F, 8, false, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+        return launch_tile_scan<T, A, C, F, 8, false, 0, false, kWG, false>(in, out, hist, nframes, k, st);
+      if (C > 1 && halo_bytes <= 16384 && tile_lds(4) <= kB)
+        return launch_tile_scan<T, A, C, F, 4, false, 0, false, kWG, false>(in, out, hist, nframes, k, st);
     } else {
-      if (C == 1 && halo_bytes <= 512 && tile_lds(4) <= kB)
-        return launch_tile_scan<T, A, C, F, 4, false, kNt>(in, out, hist, nframes, k, st, kRemapGroup);
+      if (C == 1 && halo_bytes <= 512 && tile_lds(2) <= kB)
+        return launch_tile_scan<T, A, C, F, 2, false, kNt, false, kWG, true>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 4096 && tile_lds(2) <= kB)
-        return launch_tile_scan<T, A, C, F, 2, false, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+        return launch_tile_scan<T, A, C, F, 2, false, 0, false, kWG, true>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 16384 && tile_lds(8) <= kB)
-        return launch_tile_scan<T, A, C, F, 8, false, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+        return launch_tile_scan<T, A, C, F, 8, false, 0, false, kWG, true>(in, out, hist, nframes, k, st);
     }
     if (segment_ring_fits<T, A, C, F>(k)) return launch_segment_rule<T, A, C, F, false>(in, out, hist, nframes, k, st);
     return launch_lookback_scan<T, A, C, F, 2, 0>(in, out, hist, nframes, k, st, ws);

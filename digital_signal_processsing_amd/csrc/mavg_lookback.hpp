@@ -233,24 +233,20 @@ __global__ __launch_bounds__(kWG) void lookback_scan_kernel(LookbackParams p) {
   __syncthreads();
 
   // ---- carry + earlier segments; outputs ----
+  // segment prefixes by one exclusive wave scan of the totals (mavg_tile.hpp)
+  static_assert(NSEG <= 64, "segment totals are scanned across one wave");
+  const int wu = __builtin_amdgcn_readfirstlane(w);
   A base[U][C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     A w0 = (A)0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) w0 += hsum[i * C + c];
+    const SA tv = lane < NSEG ? tot[lane * C + c] : (SA)0;
+    const SA ex = wave_incl_scan(tv) - tv;
 #pragma unroll
-    for (int u = 0; u < U; ++u) base[u][c] = w0;
+    for (int u = 0; u < U; ++u) base[u][c] = w0 + (A)readlane(ex, u * NW + wu);
   }
-#pragma unroll
-  for (int sg = 0; sg < NSEG; ++sg)
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const A t = (A)tot[sg * C + c];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (sg < u * NW + w) base[u][c] += t;
-    }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const long long f = t0 + (long long)(u * WG + tid) * F;

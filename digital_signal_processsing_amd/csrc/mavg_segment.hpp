@@ -229,28 +229,21 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
     // (c) one barrier per chunk
     __syncthreads();
 
-    // (d) segment prefixes -> window sums -> outputs
+    // (d) segment prefixes -> window sums -> outputs: lane i holds wave
+    // segment i's total, one exclusive wave scan gives every prefix, each unit
+    // reads its own with a uniform readlane (mavg_tile.hpp, same idea)
+    static_assert(NSEG <= 64, "segment totals are scanned across one wave");
+    const int wu = __builtin_amdgcn_readfirstlane(w);
     A base[U][C];
-    A total[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) total[c] = (A)0;
+    for (int c = 0; c < C; ++c) {
+      const A tv = lane < NSEG ? tot[(par * NSEG + lane) * C + c] : (A)0;
+      const A incl = wave_incl_scan(tv);
+      const A ex = incl - tv;
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int c = 0; c < C; ++c) base[u][c] = carry[c];
-#pragma unroll
-    for (int s = 0; s < NSEG; ++s) {
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const A t = tot[(par * NSEG + s) * C + c];
-        total[c] += t;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (s < u * kNW + w) base[u][c] += t;
-      }
+      for (int u = 0; u < U; ++u) base[u][c] = carry[c] + readlane(ex, u * kNW + wu);
+      carry[c] += readlane(incl, NSEG - 1);
     }
-#pragma unroll
-    for (int c = 0; c < C; ++c) carry[c] += total[c];
 
     if (ci >= p.pre_chunks) {
       const bool full = (c0 + CHF <= s1);

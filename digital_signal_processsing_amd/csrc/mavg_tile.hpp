@@ -37,8 +37,13 @@ struct TileParams {
 // tile was just loaded by this workgroup, the halo by the previous tile's
 // workgroup on the same XCD) instead of staging them in LDS; LDS then holds
 // only the scan totals, so the tile size no longer depends on k.
+// RC (Blelloch flavour, LDS-staged): keep only each lane's total across the
+// second barrier and rebuild the in-lane prefix afterwards from the LDS stage
+// (the tile and x[n-k] are both staged), in the same order, so outputs are
+// bitwise the same while U*F*C accumulators and the U tile units leave the
+// register file (e.g. 122 -> ~60 VGPRs for fp32 U=8: occupancy 4 -> 8 waves).
 template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, bool GX = false,
-          int WG = kWG>
+          int WG = kWG, bool RC = true>
 __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
@@ -146,10 +151,50 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   // (6 steps per element, O(n log n) work) with a scalar carry across the F
   // registers; x and x[n-k] both come from the LDS stage.
   constexpr bool kHsT = HS && !GX;
-  A v[U][F][C];
+  constexpr bool kRC = RC && !HS && !GX;
+  // x[n-k] for lane unit j, from the LDS stage
+  auto stage_xk = [&](int j) -> U_t {
+    const int e = (Ha + j * F - k) * C;
+    U_t xk;
+    if constexpr (IO::kVec) {
+      if (p.xk_off == 0) {
+        xk = IO::load(stage + e);
+      } else {
+        const int e_lo = e - p.xk_off;
+        U_t a = IO::load(stage + e_lo);
+        U_t b = IO::load(stage + e_lo + VE);
+        xk = extract(a, b, p.xk_off);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < VE; ++i) xk.e[i] = stage[e + i];
+    }
+    return xk;
+  };
+  A v[kRC ? 1 : U][F][C];
   A lx[U][C];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
+    if constexpr (kRC) {
+      const int j = u * WG + tid;
+      const U_t xu = IO::load(stage + (Hu + j) * VE);  // x's registers died at the stage store
+      const U_t xk = stage_xk(j);
+      A run[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) run[c] = (A)0;
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c) run[c] += to_acc<A>(xu.e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const A incl = wave_incl_scan(run[c]);
+        lx[u][c] = incl - run[c];
+        const A segtot = readlane(incl, 63);
+        if (lane == 0) tot[(u * NW + w) * C + c] = segtot;
+      }
+      continue;
+    }
     if constexpr (kHsT) {
       const int sb = (u * WG + w * 64) * F;  // tile-local first frame of this wave segment
       A run[C];
@@ -270,24 +315,23 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   __syncthreads();
 
   // ---- carry: halo sum + earlier segments; outputs ----
+  // segment s = u*NW + w needs the sum of the totals of segments < s: lane i
+  // loads total i, one exclusive wave scan gives every prefix, and each unit
+  // reads its own with a uniform readlane (NSEG <= 64), instead of every
+  // lane reading all NSEG totals
+  static_assert(NSEG <= 64, "segment totals are scanned across one wave");
+  const int wu = __builtin_amdgcn_readfirstlane(w);
   A base[U][C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     A w0 = (A)0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) w0 += hsum[i * C + c];
+    const A tv = lane < NSEG ? tot[lane * C + c] : (A)0;
+    const A ex = wave_incl_scan(tv) - tv;
 #pragma unroll
-    for (int u = 0; u < U; ++u) base[u][c] = w0;
+    for (int u = 0; u < U; ++u) base[u][c] = w0 + readlane(ex, u * NW + wu);
   }
-#pragma unroll
-  for (int s = 0; s < NSEG; ++s)
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const A t = tot[s * C + c];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (s < u * NW + w) base[u][c] += t;
-    }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if constexpr (kHsT) {
@@ -303,10 +347,26 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
     }
     const long long f = t0 + (long long)(u * WG + tid) * F;
     U_t y;
+    if constexpr (kRC) {
+      const int j = u * WG + tid;
+      const U_t xu = IO::load(stage + (Hu + j) * VE);
+      const U_t xk = stage_xk(j);
+      A run[C];
 #pragma unroll
-    for (int fr = 0; fr < F; ++fr)
+      for (int c = 0; c < C; ++c) run[c] = (A)0;
 #pragma unroll
-      for (int c = 0; c < C; ++c) y.e[fr * C + c] = to_out<T, A>(base[u][c] + lx[u][c] + v[u][fr][c], p.o);
+      for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          run[c] += to_acc<A>(xu.e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
+          y.e[fr * C + c] = to_out<T, A>(base[u][c] + lx[u][c] + run[c], p.o);
+        }
+    } else {
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c) y.e[fr * C + c] = to_out<T, A>(base[u][c] + lx[u][c] + v[u][fr][c], p.o);
+    }
     if (tile_full) {
       IO::template store<(NT & kNtStore) != 0>(out + f * C, y);
     } else {

@@ -237,6 +237,13 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   vs.push_back({"hillis tile U1", true, [=](hipStream_t s) {
                   return launch_tile_scan<float, double, 1, 4, 1, true, 0, false>(x, y, nullptr, n, k, s);
                 }});
+#define TILENR(U, NT)                                                                                   \
+  vs.push_back({"tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                                 \
+                  return launch_tile_scan<float, double, 1, 4, U, false, NT, false, 256, false>(x, y, nullptr, n, k, s); \
+                }});
+  TILENR(2, 0)
+  TILENR(4, 3)
+  TILENR(8, 0)
   // clean grid for the dispatch rules (tools/tune/sweep_shapes.sh)
 #define LB(U)                                                                                           \
   vs.push_back({"lookback U" #U, true, [=](hipStream_t s) {                                               \
@@ -322,6 +329,12 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
     SLB(1)
     SLB(2)
     SLB(4)
+#define STILENR(U, NT)                                                                                  \
+  vs.push_back({"i16 stereo tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                      \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, false, 256, false>(x, y, nullptr, n / 2, k, s); \
+                }});
+    STILENR(4, 3)
+    STILENR(4, 0)
     STILE(2, 0, 64)
     STILE(2, 3, 64)
     STILE(4, 0, 64)
@@ -343,6 +356,12 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   ILB(1)
   ILB(2)
   ILB(4)
+#define ITILENR(U, NT)                                                                                  \
+  vs.push_back({"i16 tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                             \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, false, 256, false>(x, y, nullptr, n, k, s); \
+                }});
+  ITILENR(4, 3)
+  ITILENR(8, 0)
   ITILENTR(2, 0, 64)
   ITILENTR(2, 3, 64)
   ITILENTR(4, 0, 64)
