@@ -28,6 +28,7 @@ __all__ = [
     "workspace_bytes",
     "resolve_algo",
     "plan",
+    "stream_copy",
     "ALGOS",
     "MavgError",
     "MavgLibraryError",
@@ -156,3 +157,13 @@ def fill_synthetic(n: int, dtype=None, seed: int = 0x5EED, offset: int = 0, dist
                                          dist, _stream_handle(stream, out.device))
     _lib.check(st, "mavg_fill_synthetic")
     return out
+
+
+def stream_copy(src, dst, stream=None) -> None:
+    """HBM calibration: dst = src with the library's flat non-temporal copy
+    kernel (not part of the filter; bench.py's same-box streaming ceiling)."""
+    nbytes = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() != nbytes:
+        raise ValueError("src and dst must have the same size in bytes")
+    st = _lib.load().mavg_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, _stream_handle(stream, src.device))
+    _lib.check(st, "mavg_stream_copy")

@@ -54,6 +54,7 @@ EXPORTED_SYMBOLS = (
     "mavg_resolve_algo",
     "mavg_plan",
     "mavg_fill_synthetic",
+    "mavg_stream_copy",
     "mavg_strerror",
     "mavg_algo_name",
     "mavg_abi_version",
@@ -100,6 +101,8 @@ def load() -> ctypes.CDLL:
     lib.mavg_strerror.restype = ctypes.c_char_p
     lib.mavg_algo_name.argtypes = [i]
     lib.mavg_algo_name.restype = ctypes.c_char_p
+    lib.mavg_stream_copy.argtypes = [vp, vp, sz, vp]
+    lib.mavg_stream_copy.restype = i
     lib.mavg_abi_version.argtypes = []
     lib.mavg_abi_version.restype = i
     _lib = lib

@@ -195,4 +195,16 @@ int mavg_fill_synthetic(void* d_out, size_t n_samples, int dtype, uint64_t seed,
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
+int mavg_stream_copy(const void* d_in, void* d_out, size_t bytes, void* stream) {
+  if (bytes == 0) return MAVG_OK;
+  if (d_in == nullptr || d_out == nullptr || bytes % 16 != 0) return MAVG_ERR_INVALID_ARG;
+  if (!aligned16(d_in) || !aligned16(d_out)) return MAVG_ERR_MISALIGNED;
+  const long long n = (long long)(bytes / 16);
+  const long long grid = (n + kWG - 1) / kWG;
+  if (grid > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(stream_copy_kernel<u32x4>, dim3((unsigned)grid), dim3(kWG), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const u32x4*>(d_in), static_cast<u32x4*>(d_out), n);
+  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+}
+
 }  // extern "C"

@@ -47,4 +47,15 @@ __global__ __launch_bounds__(kWG) void synth_kernel(T* __restrict__ out, long lo
   }
 }
 
+// ----------------------------------------------------------------------------
+// HBM calibration copy (mavg_stream_copy): one 16-B non-temporal load and
+// store per thread over a flat grid -- the fastest copy shape measured
+// (tools/tune/membw.hip)
+// ----------------------------------------------------------------------------
+template <typename V>
+__global__ __launch_bounds__(kWG) void stream_copy_kernel(const V* __restrict__ in, V* __restrict__ out, long long n) {
+  const long long i = (long long)blockIdx.x * kWG + threadIdx.x;
+  if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load(in + i), out + i);
+}
+
 }  // namespace mavg

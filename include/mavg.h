@@ -115,6 +115,13 @@ int mavg_resolve_algo(size_t n_samples, int channels, int grade, int dtype, int 
 int mavg_fill_synthetic(void* d_out, size_t n_samples, int dtype, uint64_t seed,
                         uint64_t offset, int dist, void* stream);
 
+/* HBM calibration (not part of the filter): d_out = d_in with one flat,
+ * non-temporal 16-B load + store per thread, the best copy measured on
+ * MI355X.  bench.py times it beside the filter so a result can be
+ * read against the same box's achievable streaming rate.  bytes a multiple
+ * of 16, both pointers 16-B aligned. */
+int mavg_stream_copy(const void* d_in, void* d_out, size_t bytes, void* stream);
+
 const char* mavg_strerror(int status);
 const char* mavg_algo_name(int algo);
 int mavg_abi_version(void);

@@ -70,6 +70,14 @@ def test_resolve_algo_is_concrete():
         assert a != _lib.ALGO_AUTO and _lib.algo_name(a) != "invalid"
 
 
+def test_stream_copy_validates():
+    lib = _lib.load()
+    assert lib.mavg_stream_copy(None, None, 0, None) == _lib.OK
+    assert lib.mavg_stream_copy(None, 16, 32, None) == _lib.ERR_INVALID_ARG
+    assert lib.mavg_stream_copy(16, 32, 24, None) == _lib.ERR_INVALID_ARG   # not a multiple of 16
+    assert lib.mavg_stream_copy(8, 32, 32, None) == _lib.ERR_MISALIGNED
+
+
 def test_fill_synthetic_validates():
     lib = _lib.load()
     assert lib.mavg_fill_synthetic(None, 0, _lib.F32, 1, 0, 0, None) == _lib.OK
