@@ -412,3 +412,46 @@ def test_lookback_large_stereo_slices(oracle_mod, gpu):
         xs = oracle_mod.synth_i16((s + span - a) * C, seed=seed, offset=a * C)
         ref = oracle_mod.mavg_i16(xs, k, C)[(s - a) * C:]
         assert np.array_equal(y[s * C:(s + span) * C], ref), f"slice at frame {s}"
+
+
+# ---------------------------------------------------------------------------
+# dispatch boundaries: windows one frame either side of every halo-size
+# threshold of dispatch_scan_f (tile shapes, tile -> segment -> look-back)
+def _boundary_windows(C, elem):
+    ks = set()
+    for h in (256, 512, 4096, 8192, 16384, 24 * 1024, 48 * 1024, 64 * 1024):
+        k0 = max(1, h // (C * elem))
+        ks.update({k0 - 1, k0, k0 + 1})
+    return sorted(k for k in ks if 10 <= k <= 40_000)
+
+
+@pytest.mark.parametrize("C", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("dtype", ["i16", "f32"])
+def test_dispatch_boundaries(oracle_mod, gpu, C, dtype):
+    import digital_signal_processsing_amd as dsp
+    rng = np.random.default_rng(1000 * C + (dtype == "f32"))
+    elem = 4 if dtype == "f32" else 2
+    seen = set()
+    for k in _boundary_windows(C, elem):
+        frames = int(rng.integers(k // 2, 3 * k + 20_000))
+        off = int(rng.integers(0, 1 << 20))
+        plan = dsp.plan(frames * C, k, C, dsp.F32 if dtype == "f32" else dsp.I16)
+        seen.add(plan.split(" grid")[0])
+        use_hist = bool(rng.integers(0, 2))
+        if dtype == "i16":
+            x = oracle_mod.synth_i16((frames + k - 1) * C, offset=off)
+            full = oracle_mod.mavg_i16(x, k, C)
+        else:
+            x = oracle_mod.synth_f32((frames + k - 1) * C, offset=off, dist=1)
+            full = oracle_mod.mavg_f32(x, k, C)
+        if use_hist:  # run on the tail with the (k-1) preceding frames as history
+            y = _run(x[(k - 1) * C:], k, C, "auto", gpu, history=x[: (k - 1) * C])
+            ref = full[(k - 1) * C:]
+        else:
+            y = _run(x[: frames * C], k, C, "auto", gpu)
+            ref = (oracle_mod.mavg_i16 if dtype == "i16" else oracle_mod.mavg_f32)(x[: frames * C], k, C)
+        if dtype == "i16":
+            assert np.array_equal(y, ref), (k, frames, use_hist, plan)
+        else:
+            assert_f32_close(y, ref, f"k={k} frames={frames} hist={use_hist} {plan}")
+    assert len(seen) >= 2, seen  # the sweep crosses kernel shapes (fp32 C=8: tile, look-back)
