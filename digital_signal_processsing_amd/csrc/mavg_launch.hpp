@@ -115,8 +115,8 @@ int launch_scan(const void* in, void* out, const void* hist, long long nframes, 
 }
 
 // flat-tile scan: one workgroup per tile, carry rebuilt from the k-frame halo
-template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, bool GX = false,
-          int WG = kWG, bool RC = true>
+template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, int WG = kWG,
+          bool RC = true>
 int launch_tile_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
                      int xcd_remap = kRemapGroup) {
   constexpr int TF = WG * F * U;
@@ -133,19 +133,19 @@ int launch_tile_scan(const void* in, void* out, const void* hist, long long nfra
   p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
   p.xcd_remap = xcd_remap;
   p.ntiles = (nframes + TF - 1) / TF;
-  const size_t stage = GX ? 0 : ((((size_t)(p.halo_units + U * WG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15);
+  const size_t stage = (((size_t)(p.halo_units + U * WG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15;
   const size_t lds = stage + (size_t)(NSEG + WG / 64) * C * sizeof(A);
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   if (p.ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,gx=%d,rc=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
+             "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
              "remap=%d",
-             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)GX, (int)RC,
+             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC,
              p.ntiles, WG, lds, TF, xcd_remap);
     return MAVG_OK;
   }
-  hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, GX, WG, RC>), dim3((unsigned)p.ntiles), dim3(WG), lds, st,
+  hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, WG, RC>), dim3((unsigned)p.ntiles), dim3(WG), lds, st,
                      p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
@@ -245,22 +245,22 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
     // int16 (measured both ways, tools/tune/ab_rc.sh, sweep_lookback2.sh)
     if constexpr (sizeof(T) == 2) {
       if (halo_bytes <= 256 && tile_lds(2) <= kB)
-        return launch_tile_scan<T, A, C, F, 2, false, kNt, false, kWG, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, false>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 4096 && tile_lds(4) <= kB)
-        return launch_tile_scan<T, A, C, F, 4, false, kNt, false, kWG, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 4, false, kNt, kWG, false>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 8192 && tile_lds(4) <= kB)
-        return launch_tile_scan<T, A, C, F, 4, false, 0, false, kWG, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 4, false, 0, kWG, false>(in, out, hist, nframes, k, st);
       if (C == 1 && halo_bytes <= 16384 && tile_lds(8) <= kB)
-        return launch_tile_scan<T, A, C, F, 8, false, 0, false, kWG, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 8, false, 0, kWG, false>(in, out, hist, nframes, k, st);
       if (C > 1 && halo_bytes <= 16384 && tile_lds(4) <= kB)
-        return launch_tile_scan<T, A, C, F, 4, false, 0, false, kWG, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 4, false, 0, kWG, false>(in, out, hist, nframes, k, st);
     } else {
       if (C == 1 && halo_bytes <= 512 && tile_lds(2) <= kB)
-        return launch_tile_scan<T, A, C, F, 2, false, kNt, false, kWG, true>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, true>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 4096 && tile_lds(2) <= kB)
-        return launch_tile_scan<T, A, C, F, 2, false, 0, false, kWG, true>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, 0, kWG, true>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 16384 && tile_lds(8) <= kB)
-        return launch_tile_scan<T, A, C, F, 8, false, 0, false, kWG, true>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 8, false, 0, kWG, true>(in, out, hist, nframes, k, st);
     }
     if (segment_ring_fits<T, A, C, F>(k)) return launch_segment_rule<T, A, C, F, false>(in, out, hist, nframes, k, st);
     return launch_lookback_scan<T, A, C, F, 2, 0>(in, out, hist, nframes, k, st, ws);

@@ -12,13 +12,14 @@ namespace mavg {
 // of being chained between workgroups:
 //     W[t0-1] = sum_{j=t0-k}^{t0-1} x[j]            (halo reduction)
 //     W[n]    = W[t0-1] + scan_{t0..n}(x[m] - x[m-k])
-// The halo and the tile are staged in LDS (x[n-k] reads); the tile's own
-// samples stay in registers.  Workgroups are remapped so that consecutive
-// tiles run on the same XCD: the halo is the tail of the tile that XCD just
-// read, an L2 hit, and all concurrently running workgroups of an XCD touch
-// one contiguous window of HBM (row-buffer locality: the "flat" access
-// shape that reaches 82% of HBM peak for a copy, tools/tune/membw.hip).
-// Two barriers per workgroup; no inter-workgroup communication.
+// The halo and the tile are staged in LDS (x[n-k] reads).  Workgroups are
+// remapped so that consecutive tiles run on the same XCD: the halo is the
+// tail of the tile that XCD just read, an L2 hit, and all concurrently
+// running workgroups of an XCD touch one contiguous window of HBM (row-buffer
+// locality: the "flat" access shape that reaches 82% of HBM peak for a copy,
+// tools/tune/membw.hip).  Two barriers per workgroup; no inter-workgroup
+// communication.  (Reading x[n-k] and the halo from global memory instead of
+// LDS measured 5.1 vs 6.26 TB/s, profiles/r01_tuning.)
 // ----------------------------------------------------------------------------
 struct TileParams {
   const void* in;
@@ -33,30 +34,31 @@ struct TileParams {
   OutParams o;
 };
 
-// GX: read x[n-k] and the halo straight from global memory (L1/L2 hits: the
-// tile was just loaded by this workgroup, the halo by the previous tile's
-// workgroup on the same XCD) instead of staging them in LDS; LDS then holds
-// only the scan totals, so the tile size no longer depends on k.
-// RC (Blelloch flavour, LDS-staged): keep only each lane's total across the
-// second barrier and rebuild the in-lane prefix afterwards from the LDS stage
-// (the tile and x[n-k] are both staged), in the same order, so outputs are
-// bitwise the same while U*F*C accumulators and the U tile units leave the
-// register file (e.g. 122 -> ~60 VGPRs for fp32 U=8: occupancy 4 -> 8 waves).
-template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, bool GX = false,
-          int WG = kWG, bool RC = true>
+// HS: Hillis-Steele flavour.  Transposed ownership: lane l holds frames l,
+//     l+64, ..., l+64(F-1) of its 64F-frame wave segment, so every register
+//     holds 64 consecutive frames and the log-step scan runs on DPP (6 steps
+//     per element, O(n log n) work) with a scalar carry across the F registers.
+// NT: bit 0 non-temporal output stores, bit 1 non-temporal input loads.
+// RC (Blelloch flavour): keep only each lane's total across the second
+//     barrier and rebuild the in-lane prefix afterwards from the LDS stage
+//     (the tile and x[n-k] are both staged), in the same order, so the
+//     outputs are bitwise the same with U*F*C fewer live accumulators.
+template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, int WG = kWG,
+          bool RC = true>
 __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
   constexpr int TF = WG * F * U;           // tile frames
   constexpr int NSEG = U * NW;
+  constexpr bool kRC = RC && !HS;
   using IO = UnitIO<T, VE>;
   using U_t = Unit<T, VE>;
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int Hu = p.halo_units;
   const int Ha = Hu * F;                     // staged halo frames (>= k)
-  const int stage_bytes = GX ? 0 : ((((Hu + U * WG + 1) * VE * (int)sizeof(T)) + 15) & ~15);
-  T* stage = reinterpret_cast<T*>(smem);     // [Hu + U*256 + 1 pad] units (LDS-staged variant)
+  const int stage_bytes = (((Hu + U * WG + 1) * VE * (int)sizeof(T)) + 15) & ~15;
+  T* stage = reinterpret_cast<T*>(smem);     // [Hu + U*256 + 1 pad] units
   A* tot = reinterpret_cast<A*>(smem + stage_bytes);  // [NSEG][C] segment totals
   A* hsum = tot + NSEG * C;                            // [NW][C] halo partial sums
 
@@ -76,7 +78,7 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   const long long h0 = t0 - Ha;              // first staged halo frame
   const bool tile_full = (t0 + TF <= nframes);
 
-  // ---- tile -> registers (streamed once: non-temporal) and LDS ----
+  // ---- tile -> registers -> LDS ----
   U_t x[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -90,8 +92,8 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
         for (int c = 0; c < C; ++c) x[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
     }
   }
-  if constexpr (!GX) {
-    // ---- halo -> LDS (re-read of the previous tile's tail: L2) ----
+  // ---- halo -> LDS (re-read of the previous tile's tail: L2) ----
+  {
     const bool halo_fast = h0 >= 0;
     for (int j = tid; j < Hu; j += WG) {
       const long long f = h0 + (long long)j * F;
@@ -106,37 +108,25 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
       }
       IO::store(stage + j * VE, h);
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) IO::store(stage + (Hu + u * WG + tid) * VE, x[u]);
-    if (tid == 0) {
-      U_t z;
-#pragma unroll
-      for (int i = 0; i < VE; ++i) z.e[i] = (T)0;
-      IO::store(stage + (Hu + U * WG) * VE, z);   // pad unit (k < F reads one unit past the tile)
-    }
-    __syncthreads();
   }
+#pragma unroll
+  for (int u = 0; u < U; ++u) IO::store(stage + (Hu + u * WG + tid) * VE, x[u]);
+  if (tid == 0) {
+    U_t z;
+#pragma unroll
+    for (int i = 0; i < VE; ++i) z.e[i] = (T)0;
+    IO::store(stage + (Hu + U * WG) * VE, z);   // pad unit (k < F reads one unit past the tile)
+  }
+  __syncthreads();
 
   // ---- halo reduction: W[t0-1] = sum of the k frames before t0 ----
   {
     A hs[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) hs[c] = (A)0;
-    if constexpr (!GX) {
-      for (int i = Ha - k + tid; i < Ha; i += WG)
+    for (int i = Ha - k + tid; i < Ha; i += WG)
 #pragma unroll
-        for (int c = 0; c < C; ++c) hs[c] += to_acc<A>(stage[i * C + c]);
-    } else {
-      if (t0 - k >= 0) {
-        for (int i = tid; i < k; i += WG)
-#pragma unroll
-          for (int c = 0; c < C; ++c) hs[c] += to_acc<A>(in[(t0 - k + i) * C + c]);
-      } else {
-        for (int i = tid; i < k; i += WG)
-#pragma unroll
-          for (int c = 0; c < C; ++c) hs[c] += to_acc<A>(load_elem(in, hist, t0 - k + i, c, C, nframes, k));
-      }
-    }
+      for (int c = 0; c < C; ++c) hs[c] += to_acc<A>(stage[i * C + c]);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const A r = readlane(wave_incl_scan(hs[c]), 63);
@@ -144,15 +134,8 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
     }
   }
 
-  // ---- d = x - x[n-k]; in-lane, wave and segment scans ----
-  // Hillis-Steele flavour (LDS-staged): transposed ownership, lane l holds
-  // frames l, l+64, ..., l+64(F-1) of its 64F-frame wave segment, so every
-  // register holds 64 consecutive frames and the log-step scan runs on DPP
-  // (6 steps per element, O(n log n) work) with a scalar carry across the F
-  // registers; x and x[n-k] both come from the LDS stage.
-  constexpr bool kHsT = HS && !GX;
-  constexpr bool kRC = RC && !HS && !GX;
-  // x[n-k] for lane unit j, from the LDS stage
+  // x[n-k] for lane unit j, from the LDS stage (an unaligned x[n-k]: two
+  // aligned units and a uniform shift)
   auto stage_xk = [&](int j) -> U_t {
     const int e = (Ha + j * F - k) * C;
     U_t xk;
@@ -171,31 +154,13 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
     }
     return xk;
   };
-  A v[kRC ? 1 : U][F][C];
-  A lx[U][C];
+
+  // ---- d = x - x[n-k]; in-lane, wave and segment scans ----
+  A v[kRC ? 1 : U][F][C];  // in-lane prefixes (Blelloch without RC) / wave scans (HS)
+  A lx[U][C];              // exclusive prefix of the lane totals inside the wave
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if constexpr (kRC) {
-      const int j = u * WG + tid;
-      const U_t xu = IO::load(stage + (Hu + j) * VE);  // x's registers died at the stage store
-      const U_t xk = stage_xk(j);
-      A run[C];
-#pragma unroll
-      for (int c = 0; c < C; ++c) run[c] = (A)0;
-#pragma unroll
-      for (int fr = 0; fr < F; ++fr)
-#pragma unroll
-        for (int c = 0; c < C; ++c) run[c] += to_acc<A>(xu.e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const A incl = wave_incl_scan(run[c]);
-        lx[u][c] = incl - run[c];
-        const A segtot = readlane(incl, 63);
-        if (lane == 0) tot[(u * NW + w) * C + c] = segtot;
-      }
-      continue;
-    }
-    if constexpr (kHsT) {
+    if constexpr (HS) {
       const int sb = (u * WG + w * 64) * F;  // tile-local first frame of this wave segment
       A run[C];
 #pragma unroll
@@ -216,98 +181,34 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
         lx[u][c] = (A)0;
         if (lane == 0) tot[(u * NW + w) * C + c] = run[c];
       }
-      continue;
-    }
-    const int j = u * WG + tid;
-    const int e = (Ha + j * F - k) * C;      // LDS element of x[n-k]
-    U_t xk;
-    if constexpr (GX) {
-      const long long fk = t0 + (long long)j * F - k;    // first frame of x[n-k]
-      if (fk >= 0 && tile_full) {   // full tile: the straddle read stays below t0 + TF - k + VE
-        if constexpr (IO::kVec) {
-          if (p.xk_off == 0) {
-            xk = IO::load(in + fk * C);
-          } else {
-            const long long e_lo = fk * C - p.xk_off;
-            U_t a = IO::load(in + e_lo);
-            U_t b = IO::load(in + e_lo + VE);
-            xk = extract(a, b, p.xk_off);
-          }
-        } else {
+    } else {
+      const int j = u * WG + tid;
+      const U_t xk = stage_xk(j);
+      A run[C];
+      if constexpr (kRC) {
+        const U_t xu = IO::load(stage + (Hu + j) * VE);  // x's registers died at the stage store
 #pragma unroll
-          for (int i = 0; i < VE; ++i) xk.e[i] = in[fk * C + i];
-        }
+        for (int c = 0; c < C; ++c) run[c] = (A)0;
+#pragma unroll
+        for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+          for (int c = 0; c < C; ++c) run[c] += to_acc<A>(xu.e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
       } else {
 #pragma unroll
         for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-          for (int c = 0; c < C; ++c) xk.e[fr * C + c] = load_elem(in, hist, fk + fr, c, C, nframes, k);
+          for (int c = 0; c < C; ++c) {
+            const A d = to_acc<A>(x[u].e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
+            v[u][fr][c] = fr == 0 ? d : v[u][fr - 1][c] + d;
+          }
+#pragma unroll
+        for (int c = 0; c < C; ++c) run[c] = v[u][F - 1][c];
       }
-    } else if constexpr (IO::kVec) {
-      if (p.xk_off == 0) {
-        xk = IO::load(stage + e);
-      } else {
-        const int e_lo = e - p.xk_off;
-        U_t a = IO::load(stage + e_lo);
-        U_t b = IO::load(stage + e_lo + VE);
-        xk = extract(a, b, p.xk_off);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < VE; ++i) xk.e[i] = stage[e + i];
-    }
-#pragma unroll
-    for (int fr = 0; fr < F; ++fr)
-#pragma unroll
-      for (int c = 0; c < C; ++c)
-        v[u][fr][c] = to_acc<A>(x[u].e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
-    if constexpr (!HS) {
-#pragma unroll
-      for (int fr = 1; fr < F; ++fr)
-#pragma unroll
-        for (int c = 0; c < C; ++c) v[u][fr][c] += v[u][fr - 1][c];
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const A t = v[u][F - 1][c];
-        const A incl = wave_incl_scan(t);
-        lx[u][c] = incl - t;
+        const A incl = wave_incl_scan(run[c]);
+        lx[u][c] = incl - run[c];
         const A segtot = readlane(incl, 63);
-        if (lane == 0) tot[(u * NW + w) * C + c] = segtot;
-      }
-    } else {
-#pragma unroll
-      for (int s = 1; s < F; s <<= 1) {
-        A t[F][C];
-#pragma unroll
-        for (int fr = 0; fr < F; ++fr)
-#pragma unroll
-          for (int c = 0; c < C; ++c) {
-            if (fr >= s) {
-              t[fr][c] = v[u][fr - s][c];
-            } else {
-              const A nbv = shfl_up(v[u][fr - s + F][c], 1);
-              t[fr][c] = lane >= 1 ? nbv : (A)0;
-            }
-          }
-#pragma unroll
-        for (int fr = 0; fr < F; ++fr)
-#pragma unroll
-          for (int c = 0; c < C; ++c) v[u][fr][c] += t[fr][c];
-      }
-#pragma unroll
-      for (int m = 1; m < 64; m <<= 1) {
-#pragma unroll
-        for (int fr = 0; fr < F; ++fr)
-#pragma unroll
-          for (int c = 0; c < C; ++c) {
-            const A nbv = shfl_up(v[u][fr][c], m);
-            v[u][fr][c] += lane >= m ? nbv : (A)0;
-          }
-      }
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        lx[u][c] = (A)0;
-        const A segtot = readlane(v[u][F - 1][c], 63);
         if (lane == 0) tot[(u * NW + w) * C + c] = segtot;
       }
     }
@@ -334,7 +235,7 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if constexpr (kHsT) {
+    if constexpr (HS) {
       const long long sb = t0 + (long long)(u * WG + w * 64) * F;
 #pragma unroll
       for (int r = 0; r < F; ++r) {

@@ -50,8 +50,7 @@ def plan_key(plan):
     hs = "true" if flavour and flavour[0] == "hillis" else "false"
     wg = re.search(r"block=(\d+)", plan).group(1)
     if fam == "tile_scan":
-        args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["nt"], "true" if kv["gx"] == "1" else "false", wg,
-                "true" if kv.get("rc", "1") == "1" else "false")
+        args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["nt"], wg, "true" if kv.get("rc", "1") == "1" else "false")
     elif fam == "direct":
         args = (T, acc, kv["C"], kv["F"], kv["U"], wg)
     elif fam == "segment_scan":

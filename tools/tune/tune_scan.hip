@@ -204,17 +204,13 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   vs.push_back({"tile U" #U " NT" #NT " remap" #RM, true, [=](hipStream_t s) {                             \
                   return launch_tile_scan<float, double, 1, 4, U, false, NT>(x, y, nullptr, n, k, s, RM);   \
                 }});
-#define TILEG(U, NT)                                                                                     \
-  vs.push_back({"tileG U" #U " NT" #NT, true, [=](hipStream_t s) {                                        \
-                  return launch_tile_scan<float, double, 1, 4, U, false, NT, true>(x, y, nullptr, n, k, s, 1); \
-                }});
 #define DIRECT(U, WG)                                                                                   \
   vs.push_back({"direct U" #U " wg" #WG, true, [=](hipStream_t s) {                                        \
                   return launch_direct<float, double, 1, 4, U, WG>(x, y, nullptr, n, k, s, 1);             \
                 }});
 #define TILEW(U, WG)                                                                                    \
   vs.push_back({"tile U" #U " wg" #WG, true, [=](hipStream_t s) {                                         \
-                  return launch_tile_scan<float, double, 1, 4, U, false, 0, false, WG>(x, y, nullptr, n, k, s, 1); \
+                  return launch_tile_scan<float, double, 1, 4, U, false, 0, WG>(x, y, nullptr, n, k, s, 1); \
                 }});
 #define SEGR(U, PD, NT, SC)                                                                              \
   vs.push_back({"seg U" #U " PD" #PD " NT" #NT " sc" #SC " remap", true, [=](hipStream_t s) {              \
@@ -225,21 +221,21 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
                 }});
 #define TILEM(U, M)                                                                                     \
   vs.push_back({"tile U" #U " remap" #M, true, [=](hipStream_t s) {                                       \
-                  return launch_tile_scan<float, double, 1, 4, U, false, 0, false>(x, y, nullptr, n, k, s, M); \
+                  return launch_tile_scan<float, double, 1, 4, U, false, 0>(x, y, nullptr, n, k, s, M); \
                 }});
 #define DIRECTM(M)                                                                                      \
   vs.push_back({"direct U1 remap" #M, true, [=](hipStream_t s) {                                          \
                   return launch_direct<float, double, 1, 4, 1>(x, y, nullptr, n, k, s, M);                 \
                 }});
   vs.push_back({"hillis tile U2", true, [=](hipStream_t s) {
-                  return launch_tile_scan<float, double, 1, 4, 2, true, 0, false>(x, y, nullptr, n, k, s);
+                  return launch_tile_scan<float, double, 1, 4, 2, true, 0>(x, y, nullptr, n, k, s);
                 }});
   vs.push_back({"hillis tile U1", true, [=](hipStream_t s) {
-                  return launch_tile_scan<float, double, 1, 4, 1, true, 0, false>(x, y, nullptr, n, k, s);
+                  return launch_tile_scan<float, double, 1, 4, 1, true, 0>(x, y, nullptr, n, k, s);
                 }});
 #define TILENR(U, NT)                                                                                   \
   vs.push_back({"tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                                 \
-                  return launch_tile_scan<float, double, 1, 4, U, false, NT, false, 256, false>(x, y, nullptr, n, k, s); \
+                  return launch_tile_scan<float, double, 1, 4, U, false, NT, 256, false>(x, y, nullptr, n, k, s); \
                 }});
   TILENR(2, 0)
   TILENR(4, 3)
@@ -296,15 +292,15 @@ template <>
 void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_t* y, long long n, int k) {
 #define ITILE(U, M)                                                                                       \
   vs.push_back({"i16 tile U" #U " remap" #M, true, [=](hipStream_t s) {                                    \
-                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, 0, false>(x, y, nullptr, n, k, s, M); \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, 0>(x, y, nullptr, n, k, s, M); \
                 }});
 #define ITILENT(U, NT)                                                                                    \
   vs.push_back({"i16 tile U" #U " NT" #NT, true, [=](hipStream_t s) {                                      \
-                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, false>(x, y, nullptr, n, k, s, 1); \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT>(x, y, nullptr, n, k, s, 1); \
                 }});
 #define ITILENTR(U, NT, M)                                                                                \
   vs.push_back({"i16 tile U" #U " NT" #NT " remap" #M, true, [=](hipStream_t s) {                          \
-                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, false>(x, y, nullptr, n, k, s, M); \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT>(x, y, nullptr, n, k, s, M); \
                 }});
 #define IPROD()                                                                                           \
   vs.push_back({"i16 product mavg_run", true, [=](hipStream_t s) {                                        \
@@ -316,7 +312,7 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                 }});
 #define STILE(U, NT, M)                                                                                   \
   vs.push_back({"i16 stereo tile U" #U " NT" #NT " remap" #M, true, [=](hipStream_t s) {                   \
-                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, false>(x, y, nullptr, n / 2, k, s, M); \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT>(x, y, nullptr, n / 2, k, s, M); \
                 }});
   if (g_channels == 2) {
     vs.push_back({"i16 stereo product mavg_run", true, [=](hipStream_t s) {
@@ -331,7 +327,7 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
     SLB(4)
 #define STILENR(U, NT)                                                                                  \
   vs.push_back({"i16 stereo tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                      \
-                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, false, 256, false>(x, y, nullptr, n / 2, k, s); \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, 256, false>(x, y, nullptr, n / 2, k, s); \
                 }});
     STILENR(4, 3)
     STILENR(4, 0)
@@ -358,7 +354,7 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   ILB(4)
 #define ITILENR(U, NT)                                                                                  \
   vs.push_back({"i16 tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                             \
-                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, false, 256, false>(x, y, nullptr, n, k, s); \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, 256, false>(x, y, nullptr, n, k, s); \
                 }});
   ITILENR(4, 3)
   ITILENR(8, 0)
