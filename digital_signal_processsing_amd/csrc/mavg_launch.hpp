@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <cstdint>
 #include <cstdio>
 
@@ -18,6 +19,9 @@ constexpr int kMaxChannels = 8;
 // per XCD, the 8 XCDs' runs adjacent (remap_tile in mavg_kernels.hpp)
 constexpr int kRemapGroup = 64;
 constexpr size_t kLdsBudget = 64 * 1024;  // per workgroup; keeps >= 2 workgroups per CU
+// A 1024-thread workgroup may take 80 KiB: two of them still fill a CU's 32
+// wave slots within its 160 KiB of LDS.
+constexpr size_t lds_budget(int wg) { return wg >= 1024 ? 80 * 1024 : kLdsBudget; }
 
 int device_cu_count();
 OutParams make_out_params(int k);
@@ -135,7 +139,7 @@ int launch_tile_scan(const void* in, void* out, const void* hist, long long nfra
   p.ntiles = (nframes + TF - 1) / TF;
   const size_t stage = (((size_t)(p.halo_units + U * WG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15;
   const size_t lds = stage + (size_t)(NSEG + WG / 64) * C * sizeof(A);
-  if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
+  if (lds > lds_budget(WG)) return MAVG_ERR_UNSUPPORTED;
   if (p.ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
@@ -144,6 +148,15 @@ int launch_tile_scan(const void* in, void* out, const void* hist, long long nfra
              type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC,
              p.ntiles, WG, lds, TF, xcd_remap);
     return MAVG_OK;
+  }
+  if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit: raise it once per instantiation
+    static std::once_flag once;
+    static hipError_t attr = hipSuccess;
+    std::call_once(once, [] {
+      attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_scan_kernel<T, A, C, F, U, HS, NT, WG, RC>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_budget(WG));
+    });
+    if (attr != hipSuccess) return MAVG_ERR_HIP;
   }
   hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, WG, RC>), dim3((unsigned)p.ntiles), dim3(WG), lds, st,
                      p);
@@ -222,8 +235,9 @@ bool segment_ring_fits(int k) {
 // launches; DESIGN.md "Tuning").  Tiles are 4 KiB of samples per U.
 //   Blelloch flavour, by halo bytes H = k*C*elem:
 //     int16  H <= 256: U2 nt | H <= 4 KiB: U4 nt | H <= 8 KiB: U4 |
-//            H <= 16 KiB: U8 (mono) / U4 (multi-channel)
-//     fp32   mono H <= 512: U2 nt rc | H <= 4 KiB: U2 rc | H <= 16 KiB: U8 rc
+//            H <= 16 KiB: U4 x 512 threads | H <= ~47 KiB: U2 x 1024 (80 KiB LDS)
+//     fp32   mono H <= 512: U2 nt rc | H <= 4 KiB: U2 rc | H <= 8 KiB: U2 x 512 rc |
+//            H <= 16 KiB: U4 x 512 rc | H <= ~47 KiB: U2 x 1024 rc
 //     longer windows: the segment-streaming scan while its LDS ring holds
 //     the window, then the two-pass look-back scan (needs the workspace)
 //   Hillis-Steele flavour: the halo-staged tile while it fits LDS, then the
@@ -234,33 +248,40 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
   constexpr int VE = F * C;
   constexpr int kUnitBytes = VE * (int)sizeof(T);
   const long long halo_bytes = (long long)k * C * (long long)sizeof(T);
-  auto tile_lds = [&](int U) -> long long {
+  auto tile_lds = [&](int U, int WG = kWG) -> long long {
     const long long hu = (k + F - 1) / F;
-    return (hu + (long long)U * kWG + 1) * kUnitBytes + (U * kNW + kNW) * C * (long long)sizeof(A);
+    return (hu + (long long)U * WG + 1) * kUnitBytes + (U * (WG / 64) + WG / 64) * C * (long long)sizeof(A);
   };
+  auto fits = [&](int U, int WG) { return tile_lds(U, WG) <= (long long)lds_budget(WG); };
   constexpr long long kB = (long long)kLdsBudget;
   constexpr int kNt = kNtLoad | kNtStore;
   if constexpr (!HS) {
     // RC (in-lane prefix rebuilt after the barrier): on for fp32, off for
-    // int16 (measured both ways, tools/tune/ab_rc.sh, sweep_lookback2.sh)
+    // int16 (measured both ways, tools/tune/ab_rc.sh, sweep_lookback2.sh).
+    // Longer halos take bigger workgroups: the LDS stage per workgroup then
+    // carries more waves (tools/tune/sweep_wg.sh, sweep_wg2.sh).
     if constexpr (sizeof(T) == 2) {
-      if (halo_bytes <= 256 && tile_lds(2) <= kB)
+      if (halo_bytes <= 256 && fits(2, kWG))
         return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, false>(in, out, hist, nframes, k, st);
-      if (halo_bytes <= 4096 && tile_lds(4) <= kB)
+      if (halo_bytes <= 4096 && fits(4, kWG))
         return launch_tile_scan<T, A, C, F, 4, false, kNt, kWG, false>(in, out, hist, nframes, k, st);
-      if (halo_bytes <= 8192 && tile_lds(4) <= kB)
+      if (halo_bytes <= 8192 && fits(4, kWG))
         return launch_tile_scan<T, A, C, F, 4, false, 0, kWG, false>(in, out, hist, nframes, k, st);
-      if (C == 1 && halo_bytes <= 16384 && tile_lds(8) <= kB)
-        return launch_tile_scan<T, A, C, F, 8, false, 0, kWG, false>(in, out, hist, nframes, k, st);
-      if (C > 1 && halo_bytes <= 16384 && tile_lds(4) <= kB)
-        return launch_tile_scan<T, A, C, F, 4, false, 0, kWG, false>(in, out, hist, nframes, k, st);
+      if (halo_bytes <= 16384 && fits(4, 512))
+        return launch_tile_scan<T, A, C, F, 4, false, 0, 512, false>(in, out, hist, nframes, k, st);
+      if (fits(2, 1024))
+        return launch_tile_scan<T, A, C, F, 2, false, 0, 1024, false>(in, out, hist, nframes, k, st);
     } else {
-      if (C == 1 && halo_bytes <= 512 && tile_lds(2) <= kB)
+      if (C == 1 && halo_bytes <= 512 && fits(2, kWG))
         return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, true>(in, out, hist, nframes, k, st);
-      if (halo_bytes <= 4096 && tile_lds(2) <= kB)
+      if (halo_bytes <= 4096 && fits(2, kWG))
         return launch_tile_scan<T, A, C, F, 2, false, 0, kWG, true>(in, out, hist, nframes, k, st);
-      if (halo_bytes <= 16384 && tile_lds(8) <= kB)
-        return launch_tile_scan<T, A, C, F, 8, false, 0, kWG, true>(in, out, hist, nframes, k, st);
+      if (halo_bytes <= 8192 && fits(2, 512))
+        return launch_tile_scan<T, A, C, F, 2, false, 0, 512, true>(in, out, hist, nframes, k, st);
+      if (halo_bytes <= 16384 && fits(4, 512))
+        return launch_tile_scan<T, A, C, F, 4, false, 0, 512, true>(in, out, hist, nframes, k, st);
+      if (fits(2, 1024))
+        return launch_tile_scan<T, A, C, F, 2, false, 0, 1024, true>(in, out, hist, nframes, k, st);
     }
     if (segment_ring_fits<T, A, C, F>(k)) return launch_segment_rule<T, A, C, F, false>(in, out, hist, nframes, k, st);
     return launch_lookback_scan<T, A, C, F, 2, 0>(in, out, hist, nframes, k, st, ws);

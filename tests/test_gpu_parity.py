@@ -417,12 +417,22 @@ def test_lookback_large_stereo_slices(oracle_mod, gpu):
 # ---------------------------------------------------------------------------
 # dispatch boundaries: windows one frame either side of every halo-size
 # threshold of dispatch_scan_f (tile shapes, tile -> segment -> look-back)
-def _boundary_windows(C, elem):
+def _boundary_windows(dsp, n, C, dt):
+    """Every window where the plan (kernel, tile, workgroup) changes, found by
+    bisection on mavg_plan (no GPU), as k-1, k, k+1."""
+    def shape(k):
+        p = dsp.plan(n, k, C, dt)
+        return p.split(" grid")[0] + p.split("block=")[1].split()[0]
+    grid = sorted(set(int(round(10 * 1.05 ** i)) for i in range(200) if 10 * 1.05 ** i <= 60_000))
     ks = set()
-    for h in (256, 512, 4096, 8192, 16384, 24 * 1024, 48 * 1024, 64 * 1024):
-        k0 = max(1, h // (C * elem))
-        ks.update({k0 - 1, k0, k0 + 1})
-    return sorted(k for k in ks if 10 <= k <= 40_000)
+    for a, b in zip(grid, grid[1:]):
+        if shape(a) != shape(b):
+            lo, hi = a, b
+            while hi - lo > 1:
+                mid = (lo + hi) // 2
+                lo, hi = (mid, hi) if shape(mid) == shape(a) else (lo, mid)
+            ks.update({hi - 1, hi, hi + 1})
+    return sorted(ks)
 
 
 @pytest.mark.parametrize("C", [1, 2, 3, 4, 8])
@@ -432,10 +442,11 @@ def test_dispatch_boundaries(oracle_mod, gpu, C, dtype):
     rng = np.random.default_rng(1000 * C + (dtype == "f32"))
     elem = 4 if dtype == "f32" else 2
     seen = set()
-    for k in _boundary_windows(C, elem):
+    dt = dsp.F32 if dtype == "f32" else dsp.I16
+    for k in _boundary_windows(dsp, 100_000 * C, C, dt):
         frames = int(rng.integers(k // 2, 3 * k + 20_000))
         off = int(rng.integers(0, 1 << 20))
-        plan = dsp.plan(frames * C, k, C, dsp.F32 if dtype == "f32" else dsp.I16)
+        plan = dsp.plan(frames * C, k, C, dt)
         seen.add(plan.split(" grid")[0])
         use_hist = bool(rng.integers(0, 2))
         if dtype == "i16":

@@ -240,6 +240,34 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   TILENR(2, 0)
   TILENR(4, 3)
   TILENR(8, 0)
+#define TILEWG(U, WG)                                                                                   \
+  vs.push_back({"tile U" #U " wg" #WG " rc", true, [=](hipStream_t s) {                                   \
+                  return launch_tile_scan<float, double, 1, 4, U, false, 0, WG>(x, y, nullptr, n, k, s, 64); \
+                }});
+#define TILEX(U, NT, WG, RC)                                                                            \
+  vs.push_back({"tileX U" #U " nt" #NT " wg" #WG " rc" #RC, true, [=](hipStream_t s) {                    \
+                  return launch_tile_scan<float, double, 1, 4, U, false, NT, WG, RC>(x, y, nullptr, n, k, s, 64); \
+                }});
+  TILEX(2, 0, 1024, true)
+  TILEX(1, 0, 1024, true)
+  TILEX(2, 0, 512, true)
+  TILEX(2, 0, 256, true)
+  TILEX(2, 0, 256, false)
+  TILEX(4, 0, 256, false)
+  TILEX(4, 3, 256, false)
+  TILEX(4, 3, 256, true)
+  TILEX(4, 1, 256, true)
+  TILEX(2, 1, 256, true)
+  TILEX(8, 3, 256, true)
+  TILEX(4, 0, 128, true)
+  TILEX(8, 0, 128, true)
+  TILEX(4, 0, 128, false)
+  TILEWG(8, 256)
+  TILEWG(4, 256)
+  TILEWG(4, 512)
+  TILEWG(2, 1024)
+  TILEWG(2, 256)
+  TILEWG(2, 512)
   // clean grid for the dispatch rules (tools/tune/sweep_shapes.sh)
 #define LB(U)                                                                                           \
   vs.push_back({"lookback U" #U, true, [=](hipStream_t s) {                                               \
@@ -325,6 +353,16 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
     SLB(1)
     SLB(2)
     SLB(4)
+#define STILEWG(U, WG, RC)                                                                              \
+  vs.push_back({"i16 stereo tile U" #U " wg" #WG " rc" #RC, true, [=](hipStream_t s) {                    \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, 0, WG, RC>(x, y, nullptr, n / 2, k, s, 64); \
+                }});
+    STILEWG(4, 256, false)
+    STILEWG(2, 512, false)
+    STILEWG(4, 512, false)
+    STILEWG(2, 1024, false)
+    STILEWG(1, 1024, false)
+    STILEWG(4, 512, true)
 #define STILENR(U, NT)                                                                                  \
   vs.push_back({"i16 stereo tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                      \
                   return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, 256, false>(x, y, nullptr, n / 2, k, s); \
@@ -345,6 +383,17 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                   }});
     return;
   }
+#define ITILEWG(U, WG, RC)                                                                              \
+  vs.push_back({"i16 tile U" #U " wg" #WG " rc" #RC, true, [=](hipStream_t s) {                           \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, 0, WG, RC>(x, y, nullptr, n, k, s, 64); \
+                }});
+  ITILEWG(8, 256, false)
+  ITILEWG(4, 256, false)
+  ITILEWG(4, 512, false)
+  ITILEWG(2, 512, false)
+  ITILEWG(4, 512, true)
+  ITILEWG(2, 1024, false)
+  ITILEWG(1, 1024, false)
 #define ILB(U)                                                                                          \
   vs.push_back({"i16 lookback U" #U, true, [=](hipStream_t s) {                                           \
                   return launch_lookback_scan<int16_t, int32_t, 1, 8, U, 0>(x, y, nullptr, n, k, s, g_ws);     \
