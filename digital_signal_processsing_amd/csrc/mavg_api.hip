@@ -79,18 +79,20 @@ const char* mavg_algo_name(int algo) {
   }
 }
 
-// AUTO: the direct register-window kernel for tiny windows (its per-output
-// cost is O(k/F); at k <= 9 a lane reads at most 3 LDS units and it measured
-// 6.27 TB/s at k=7 vs 6.18 for the tile scan), the flat-tile Blelloch scan
-// otherwise (O(1) per output for any k).  Both move 1.00x the algorithmic
-// bytes on HBM (profiles/).
+// AUTO: the Blelloch scan family at every window (flat tiles with the tile
+// shape chosen by dispatch_scan_f; O(1) work per output for any k).  The
+// direct kernel is kept for MAVG_ALGO_DIRECT*: since the tile scan's carry
+// became a wave scan of the segment totals, tiles beat it even at k <= 9
+// (k=7, 2^28 samples: fp32 0.821 vs 0.797 of HBM peak, int16 0.795 vs 0.761,
+// tools/tune/tune_scan.hip).  Both move 1.00x the algorithmic bytes on HBM.
 // More than kMaxChannels channels: only the naive kernel (runtime C) applies.
 int mavg_resolve_algo(size_t n_samples, int channels, int grade, int dtype, int algo) {
   (void)n_samples;
   (void)dtype;
+  (void)grade;
   if (algo != MAVG_ALGO_AUTO) return algo;
   if (channels > kMaxChannels) return MAVG_ALGO_NAIVE;
-  return grade <= 9 ? MAVG_ALGO_DIRECT : MAVG_ALGO_BLELLOCH;
+  return MAVG_ALGO_BLELLOCH;
 }
 
 int mavg_workspace_bytes(size_t n_samples, int channels, int grade, int dtype, int algo, int block_size,

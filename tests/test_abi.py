@@ -136,10 +136,11 @@ def test_lookback_without_workspace_is_an_error():
     assert st == _lib.ERR_WORKSPACE
 
 
-def test_auto_picks_direct_for_tiny_windows():
+def test_auto_picks_the_tile_scan_at_every_window():
     import digital_signal_processsing_amd as dsp
-    assert dsp.resolve_algo(1 << 20, 7) == "direct" and dsp.resolve_algo(1 << 20, 9) == "direct"
-    assert dsp.resolve_algo(1 << 20, 10) == "blelloch" and dsp.resolve_algo(1 << 20, 1024) == "blelloch"
+    for k in (1, 7, 9, 10, 1024, 100_000):
+        assert dsp.resolve_algo(1 << 20, k) == "blelloch", k
+    assert dsp.plan(1 << 20, 7, algo="direct").startswith("direct<")
 
 
 def test_many_channels_auto_resolves_to_naive():

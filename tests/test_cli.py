@@ -156,3 +156,20 @@ def test_harness_quick_sweep_verifies_every_variant(tmp_path):
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, universal_newlines=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert "Total Failures/Crashes: 0" in r.stdout and "Output mismatches vs bin_cpu: 0" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["bin_vblelloch", "bin_blelloch"])
+def test_gpu_bins_long_windows(tmp_path, oracle_mod, name):
+    """One-second windows at 44.1 kHz and beyond: the 1024-thread tile and the
+    look-back scan, whose workspace comes from the CLI's DspWorkspace scratch,
+    in both memory modes (Standard, Unified = managed scratch too)."""
+    rng = np.random.default_rng(11)
+    data = rng.integers(-32768, 32767, size=(150_001, 2), dtype=np.int16)
+    path = tmp_path / "long.wav"
+    rb.write_wav(str(path), data)
+    for grade in (5000, 44100, 70000):
+        r = _run(name, path, grade, 256, "--out", tmp_path / "o.wav", cwd=tmp_path)
+        assert r.returncode == 0, r.stdout + r.stderr
+        y = rb.read_wav_samples(str(tmp_path / "o.wav"))
+        assert np.array_equal(y, oracle_mod.mavg_i16(data.reshape(-1), grade, 2)), (name, grade)
