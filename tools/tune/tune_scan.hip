@@ -248,6 +248,9 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   vs.push_back({"tileX U" #U " nt" #NT " wg" #WG " rc" #RC, true, [=](hipStream_t s) {                    \
                   return launch_tile_scan<float, double, 1, 4, U, false, NT, WG, RC>(x, y, nullptr, n, k, s, 64); \
                 }});
+  TILEX(2, 1, 256, false)
+  TILEX(2, 0, 512, false)
+  TILEX(2, 1, 512, true)
   TILEX(2, 0, 1024, true)
   TILEX(1, 0, 1024, true)
   TILEX(2, 0, 512, true)
