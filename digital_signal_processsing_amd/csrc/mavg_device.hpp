@@ -224,5 +224,10 @@ __device__ __forceinline__ long long remap_tile(unsigned b, unsigned nb, int mod
 // non-temporal (streamed-once) policy bits of the NT template parameters
 constexpr int kNtStore = 1;
 constexpr int kNtLoad = 2;
+// tile scan only: nt loads for the part of the tile that no later tile's
+// halo re-reads (the last halo-size frames stay plain, so the next tile finds
+// them in L2), and nt loads for the halo itself (its last use)
+constexpr int kNtSplit = 4;
+constexpr int kNtHalo = 8;
 
 }  // namespace mavg

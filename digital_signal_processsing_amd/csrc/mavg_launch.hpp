@@ -233,11 +233,13 @@ bool segment_ring_fits(int k) {
 // Algorithm selection for the scan family (measured on MI355X with
 // tools/tune/tune_scan.hip + tools/tune/sweep_*.sh, 2^30 samples, back-to-back
 // launches; DESIGN.md "Tuning").  Tiles are 4 KiB of samples per U.
-//   Blelloch flavour, by halo bytes H = k*C*elem:
-//     int16  H <= 256: U2 nt | H <= 4 KiB: U4 nt | H <= 8 KiB: U4 |
-//            H <= 16 KiB: U4 x 512 threads | H <= ~47 KiB: U2 x 1024 (80 KiB LDS)
-//     fp32   mono H <= 512: U2 nt rc | H <= 4 KiB: U2 rc | H <= 8 KiB: U2 x 512 rc |
-//            H <= 16 KiB: U4 x 512 rc | H <= ~47 KiB: U2 x 1024 rc
+//   Blelloch flavour, by halo bytes H = k*C*elem (nt: every load and store
+//   non-temporal; ntS: the split policy kNtS below):
+//     int16  H <= 256: U2 nt | H <= 4 KiB: U4 nt | H <= 8 KiB: U4 ntS |
+//            H <= 16 KiB: U4 x 512 threads ntS | H <= ~47 KiB: U2 x 1024 (80 KiB LDS) ntS
+//     fp32   mono H <= 512: U2 nt rc | H <= 4 KiB: U2 ntS rc | H <= 8 KiB: U2 x 512 ntS rc |
+//            H <= 16 KiB: U4 x 512 ntS rc | H <= ~47 KiB: U2 x 1024 ntS rc
+//     longer windows: the two-pass look-back with nt output stores
 //     longer windows: the segment-streaming scan while its LDS ring holds
 //     the window, then the two-pass look-back scan (needs the workspace)
 //   Hillis-Steele flavour: the halo-staged tile while it fits LDS, then the
@@ -255,6 +257,10 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
   auto fits = [&](int U, int WG) { return tile_lds(U, WG) <= (long long)lds_budget(WG); };
   constexpr long long kB = (long long)kLdsBudget;
   constexpr int kNt = kNtLoad | kNtStore;
+  // split policy: nt tile loads except the tail the next tile's halo re-reads,
+  // nt halo loads (their last use), nt stores (tools/tune/sweep_nt.sh: +1-4 %
+  // over default-policy loads wherever the halo is re-read from L2)
+  constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
   if constexpr (!HS) {
     // RC (in-lane prefix rebuilt after the barrier): on for fp32, off for
     // int16 (measured both ways, tools/tune/ab_rc.sh, sweep_lookback2.sh).
@@ -266,25 +272,25 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
       if (halo_bytes <= 4096 && fits(4, kWG))
         return launch_tile_scan<T, A, C, F, 4, false, kNt, kWG, false>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 8192 && fits(4, kWG))
-        return launch_tile_scan<T, A, C, F, 4, false, 0, kWG, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 4, false, kNtS, kWG, false>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 16384 && fits(4, 512))
-        return launch_tile_scan<T, A, C, F, 4, false, 0, 512, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 4, false, kNtS, 512, false>(in, out, hist, nframes, k, st);
       if (fits(2, 1024))
-        return launch_tile_scan<T, A, C, F, 2, false, 0, 1024, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, kNtS, 1024, false>(in, out, hist, nframes, k, st);
     } else {
       if (C == 1 && halo_bytes <= 512 && fits(2, kWG))
         return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, true>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 4096 && fits(2, kWG))
-        return launch_tile_scan<T, A, C, F, 2, false, 0, kWG, true>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, kNtS, kWG, true>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 8192 && fits(2, 512))
-        return launch_tile_scan<T, A, C, F, 2, false, 0, 512, true>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, kNtS, 512, true>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 16384 && fits(4, 512))
-        return launch_tile_scan<T, A, C, F, 4, false, 0, 512, true>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 4, false, kNtS, 512, true>(in, out, hist, nframes, k, st);
       if (fits(2, 1024))
-        return launch_tile_scan<T, A, C, F, 2, false, 0, 1024, true>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, kNtS, 1024, true>(in, out, hist, nframes, k, st);
     }
     if (segment_ring_fits<T, A, C, F>(k)) return launch_segment_rule<T, A, C, F, false>(in, out, hist, nframes, k, st);
-    return launch_lookback_scan<T, A, C, F, 2, 0>(in, out, hist, nframes, k, st, ws);
+    return launch_lookback_scan<T, A, C, F, 2, kNtStore>(in, out, hist, nframes, k, st, ws);
   } else {
     if constexpr (sizeof(T) == 2) {
       if (halo_bytes <= 2 * 1024 && tile_lds(4) <= kB)

@@ -46,6 +46,41 @@ struct LookbackParams {
 template <typename T, typename A> struct ScanAcc { using type = A; };
 template <> struct ScanAcc<int16_t, int64_t> { using type = int32_t; };
 
+// Stage the shifted tile [h0, h0 + (U*WG+1)*F) frames in LDS: every lane's
+// U units are loaded before any is stored (one memory round trip, not one per
+// unit), plus one extra unit for the misaligned x[n-k] read.
+template <typename T, int C, int F, int U, int WG, int NT>
+__device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, const T* __restrict__ hist,
+                                                   T* stage, long long h0, long long nframes, int k, int tid) {
+  constexpr int VE = F * C;
+  using IO = UnitIO<T, VE>;
+  using U_t = Unit<T, VE>;
+  const bool fast = h0 >= 0 && h0 + (long long)(U * WG + 1) * F <= nframes;
+  U_t h[U + 1];
+  auto guarded = [&](int j) {
+    U_t r;
+    const long long f = h0 + (long long)j * F;
+#pragma unroll
+    for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+      for (int c = 0; c < C; ++c) r.e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+    return r;
+  };
+  if (fast) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      h[u] = IO::template load<(NT & kNtHalo) != 0>(in + (h0 + (long long)(u * WG + tid) * F) * C);
+    if (tid == 0) h[U] = IO::template load<(NT & kNtHalo) != 0>(in + (h0 + (long long)(U * WG) * F) * C);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) h[u] = guarded(u * WG + tid);
+    if (tid == 0) h[U] = guarded(U * WG);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) IO::store(stage + (u * WG + tid) * VE, h[u]);
+  if (tid == 0) IO::store(stage + (U * WG) * VE, h[U]);
+}
+
 // pass 1: the sum of every whole tile (per channel), reduced per lane over
 // its units, then across the wave (DPP scan), then across the waves in order
 template <typename T, typename A, int C, int F, int U>
@@ -150,22 +185,7 @@ __global__ __launch_bounds__(kWG) void lookback_scan_kernel(LookbackParams p) {
     for (int c = 0; c < C; ++c) hq[c] += (A)sums[j * C + c];
   // ---- shifted tile [h0, h0 + kStageUnits*F) -> LDS (read k frames back:
   //      L2 / MALL) ----
-  {
-    const bool fast = h0 >= 0 && h0 + (long long)kStageUnits * F <= nframes;
-    for (int j = tid; j < kStageUnits; j += WG) {
-      const long long f = h0 + (long long)j * F;
-      U_t h;
-      if (fast) {
-        h = IO::load(in + f * C);
-      } else {
-#pragma unroll
-        for (int fr = 0; fr < F; ++fr)
-#pragma unroll
-          for (int c = 0; c < C; ++c) h.e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
-      }
-      IO::store(stage + j * VE, h);
-    }
-  }
+  stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, tid);
   __syncthreads();
 
   // ---- carry W[t0-1] = partial + whole tiles ----

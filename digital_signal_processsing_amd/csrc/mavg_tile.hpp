@@ -38,7 +38,9 @@ struct TileParams {
 //     l+64, ..., l+64(F-1) of its 64F-frame wave segment, so every register
 //     holds 64 consecutive frames and the log-step scan runs on DPP (6 steps
 //     per element, O(n log n) work) with a scalar carry across the F registers.
-// NT: bit 0 non-temporal output stores, bit 1 non-temporal input loads.
+// NT: bit 0 non-temporal output stores, bit 1 non-temporal input loads,
+//     bit 2 (kNtSplit) non-temporal tile loads except the last halo-size
+//     frames, bit 3 (kNtHalo) non-temporal halo loads.
 // RC (Blelloch flavour): keep only each lane's total across the second
 //     barrier and rebuild the in-lane prefix afterwards from the LDS stage
 //     (the tile and x[n-k] are both staged), in the same order, so the
@@ -84,7 +86,13 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   for (int u = 0; u < U; ++u) {
     const long long f = t0 + (long long)(u * WG + tid) * F;
     if (tile_full) {
-      x[u] = IO::template load<(NT & kNtLoad) != 0>(in + f * C);
+      if constexpr ((NT & kNtSplit) != 0) {
+        // frames the next tile's halo re-reads keep the default policy (L2)
+        if ((u * WG + tid) * F + F > TF - Ha) x[u] = IO::template load<false>(in + f * C);
+        else x[u] = IO::template load<true>(in + f * C);
+      } else {
+        x[u] = IO::template load<(NT & kNtLoad) != 0>(in + f * C);
+      }
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)
@@ -99,7 +107,7 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
       const long long f = h0 + (long long)j * F;
       U_t h;
       if (halo_fast) {
-        h = IO::load(in + f * C);
+        h = IO::template load<(NT & kNtHalo) != 0>(in + f * C);
       } else {
 #pragma unroll
         for (int fr = 0; fr < F; ++fr)

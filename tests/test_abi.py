@@ -96,6 +96,9 @@ def test_plan_describes_launch_without_gpu():
     import digital_signal_processsing_amd as dsp
     p = dsp.plan(1 << 30, 1024)
     assert p.startswith("tile_scan<f32,acc=f64,C=1,F=4,U=2,blelloch") and "grid=524288" in p, p
+    # split cache policy (nt tile loads but the halo tail, nt halo, nt stores)
+    assert "nt=13" in p and "nt=13" in dsp.plan(1 << 30, 4096), p
+    assert "nt=3" in dsp.plan(1 << 30, 64)  # tiny halo: everything non-temporal
     assert "U=4" in dsp.plan(1 << 30, 4096) and "block=512" in dsp.plan(1 << 30, 4096)
     assert dsp.plan(1 << 20, 70_000).startswith("lookback_scan<f32")
     assert dsp.plan(1 << 20, 70_000, algo="hillis").startswith("segment_scan<") and "xkg=1" in dsp.plan(

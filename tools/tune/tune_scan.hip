@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../digital_signal_processsing_amd/csrc/mavg_launch.hpp"
+#include "onepass_experiment.hpp"
 
 using namespace mavg;
 
@@ -161,6 +162,11 @@ int run(int lg, int k, int rounds) {
       CK(hipMemcpyAsync(&v.mism, dcnt, 8, hipMemcpyDeviceToHost, st));
     }
     CK(hipStreamSynchronize(st));
+    if (v.name.find("onepass") != std::string::npos) {
+      unsigned int fb = 0;
+      CK(hipMemcpy(&fb, g_ws.ptr, 4, hipMemcpyDeviceToHost));
+      printf("%s: record recomputes (fallbacks) = %u\n", v.name.c_str(), fb);
+    }
     CK(hipMemsetAsync(y, 0xff, n * ES, st));
   }
   for (auto& v : vs) { v.launch(st); v.launch(st); }
@@ -230,6 +236,17 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   vs.push_back({"hillis tile U2", true, [=](hipStream_t s) {
                   return launch_tile_scan<float, double, 1, 4, 2, true, 0>(x, y, nullptr, n, k, s);
                 }});
+#define HTS(U, NT, WG)                                                                                  \
+  vs.push_back({"hillisS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                              \
+                  return launch_tile_scan<float, double, 1, 4, U, true, NT, WG>(x, y, nullptr, n, k, s);     \
+                }});
+  HTS(2, 0, 256)
+  HTS(2, 1, 256)
+  HTS(2, 3, 256)
+  HTS(2, 13, 256)
+  HTS(1, 13, 256)
+  HTS(2, 13, 512)
+  HTS(4, 13, 256)
   vs.push_back({"hillis tile U1", true, [=](hipStream_t s) {
                   return launch_tile_scan<float, double, 1, 4, 1, true, 0>(x, y, nullptr, n, k, s);
                 }});
@@ -279,6 +296,45 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   LB(1)
   LB(2)
   LB(4)
+#define OP(U, NT)                                                                                       \
+  vs.push_back({"onepass U" #U " NT" #NT, true, [=](hipStream_t s) {                                      \
+                  return launch_onepass_scan<float, double, 1, 4, U, NT>(x, y, nullptr, n, k, s, g_ws);        \
+                }});
+  OP(1, 0)
+  OP(2, 0)
+  OP(4, 0)
+  OP(2, 1)
+  OP(2, 8)
+  OP(4, 8)
+#define TILES(U, NT, WG)                                                                                \
+  vs.push_back({"tileS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                               \
+                  return launch_tile_scan<float, double, 1, 4, U, false, NT, WG, true>(x, y, nullptr, n, k, s, 64); \
+                }});
+  TILES(2, 0, 256)
+  TILES(2, 1, 256)
+  TILES(2, 4, 256)
+  TILES(2, 5, 256)
+  TILES(2, 12, 256)
+  TILES(2, 13, 256)
+  TILES(4, 0, 512)
+  TILES(4, 4, 512)
+  TILES(4, 5, 512)
+  TILES(4, 13, 512)
+  TILES(4, 1, 512)
+  TILES(2, 0, 512)
+  TILES(2, 1, 512)
+  TILES(2, 5, 512)
+  TILES(2, 13, 512)
+  TILES(2, 0, 1024)
+  TILES(2, 1, 1024)
+  TILES(2, 5, 1024)
+  TILES(2, 13, 1024)
+#define LBN(U, NT)                                                                                      \
+  vs.push_back({"lookbackN U" #U " nt" #NT, true, [=](hipStream_t s) {                                     \
+                  return launch_lookback_scan<float, double, 1, 4, U, NT>(x, y, nullptr, n, k, s, g_ws);       \
+                }});
+  LBN(2, 0)
+  LBN(2, 1)
   TILE(1, 0, 64)
   TILE(2, 0, 64)
   TILE(2, 1, 64)
@@ -356,6 +412,28 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
     SLB(1)
     SLB(2)
     SLB(4)
+#define SOP(U)                                                                                          \
+  vs.push_back({"i16 stereo onepass U" #U, true, [=](hipStream_t s) {                                     \
+                  return launch_onepass_scan<int16_t, int32_t, 2, 4, U, 0>(x, y, nullptr, n / 2, k, s, g_ws); \
+                }});
+    SOP(1)
+    SOP(2)
+    SOP(4)
+#define STILES(U, NT, WG)                                                                               \
+  vs.push_back({"i16 stereo tileS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                   \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, WG, false>(x, y, nullptr, n / 2, k, s, 64); \
+                }});
+    STILES(4, 0, 256)
+    STILES(4, 3, 256)
+    STILES(4, 4, 256)
+    STILES(4, 5, 256)
+    STILES(4, 13, 256)
+    STILES(4, 0, 512)
+    STILES(4, 5, 512)
+    STILES(4, 13, 512)
+    STILES(2, 0, 1024)
+    STILES(2, 5, 1024)
+    STILES(2, 13, 1024)
 #define STILEWG(U, WG, RC)                                                                              \
   vs.push_back({"i16 stereo tile U" #U " wg" #WG " rc" #RC, true, [=](hipStream_t s) {                    \
                   return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, 0, WG, RC>(x, y, nullptr, n / 2, k, s, 64); \
@@ -404,6 +482,28 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   ILB(1)
   ILB(2)
   ILB(4)
+#define IOP(U)                                                                                          \
+  vs.push_back({"i16 onepass U" #U, true, [=](hipStream_t s) {                                            \
+                  return launch_onepass_scan<int16_t, int32_t, 1, 8, U, 0>(x, y, nullptr, n, k, s, g_ws);      \
+                }});
+  IOP(1)
+  IOP(2)
+  IOP(4)
+#define ITILES(U, NT, WG)                                                                               \
+  vs.push_back({"i16 tileS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                          \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, WG, false>(x, y, nullptr, n, k, s, 64); \
+                }});
+  ITILES(4, 0, 256)
+  ITILES(4, 3, 256)
+  ITILES(4, 4, 256)
+  ITILES(4, 5, 256)
+  ITILES(4, 13, 256)
+  ITILES(4, 0, 512)
+  ITILES(4, 5, 512)
+  ITILES(4, 13, 512)
+  ITILES(2, 0, 1024)
+  ITILES(2, 5, 1024)
+  ITILES(2, 13, 1024)
 #define ITILENR(U, NT)                                                                                  \
   vs.push_back({"i16 tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                             \
                   return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, 256, false>(x, y, nullptr, n, k, s); \
