@@ -242,7 +242,8 @@ bool segment_ring_fits(int k) {
 //     longer windows: the two-pass look-back with nt output stores
 //     longer windows: the segment-streaming scan while its LDS ring holds
 //     the window, then the two-pass look-back scan (needs the workspace)
-//   Hillis-Steele flavour: the halo-staged tile while it fits LDS, then the
+//   Hillis-Steele flavour: the halo-staged tile while it fits LDS (fp32: U4 nt
+//   for H <= 512 B, else U8 ntS; int16: U4 x 512 threads ntS), then the
 //   segment-streaming scan.
 template <typename T, typename A, int C, int F, bool HS>
 int dispatch_scan_f(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
@@ -292,17 +293,19 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
     if (segment_ring_fits<T, A, C, F>(k)) return launch_segment_rule<T, A, C, F, false>(in, out, hist, nframes, k, st);
     return launch_lookback_scan<T, A, C, F, 2, kNtStore>(in, out, hist, nframes, k, st, ws);
   } else {
+    // Hillis-Steele: the element-wise log-step scans make a tile's compute
+    // long, so bigger tiles (fewer halos and barriers per byte) and the split
+    // cache policy win (tools/tune/sweep_hillis.sh: fp32 k=1024 0.66 -> 0.78)
     if constexpr (sizeof(T) == 2) {
-      if (halo_bytes <= 2 * 1024 && tile_lds(4) <= kB)
-        return launch_tile_scan<T, A, C, F, 4, HS, kNt>(in, out, hist, nframes, k, st, kRemapGroup);
-      if (halo_bytes <= 8 * 1024 && tile_lds(4) <= kB)
-        return launch_tile_scan<T, A, C, F, 4, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+      if (fits(4, 512))
+        return launch_tile_scan<T, A, C, F, 4, HS, kNtS, 512>(in, out, hist, nframes, k, st, kRemapGroup);
     } else {
-      if (halo_bytes <= 8 * 1024 && tile_lds(2) <= kB)
-        return launch_tile_scan<T, A, C, F, 2, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+      if (C == 1 && halo_bytes <= 512 && fits(4, kWG))
+        return launch_tile_scan<T, A, C, F, 4, HS, kNt>(in, out, hist, nframes, k, st, kRemapGroup);
+      if (fits(8, kWG))
+        return launch_tile_scan<T, A, C, F, 8, HS, kNtS>(in, out, hist, nframes, k, st, kRemapGroup);
     }
-    if (tile_lds(8) <= kB)
-      return launch_tile_scan<T, A, C, F, 8, HS, 0>(in, out, hist, nframes, k, st, kRemapGroup);
+    (void)kB;
     return launch_segment_rule<T, A, C, F, HS>(in, out, hist, nframes, k, st);
   }
 }

@@ -247,6 +247,14 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   HTS(1, 13, 256)
   HTS(2, 13, 512)
   HTS(4, 13, 256)
+  HTS(4, 3, 256)
+  HTS(4, 1, 256)
+  HTS(8, 13, 256)
+  HTS(8, 3, 256)
+  HTS(4, 13, 512)
+  HTS(2, 3, 512)
+  HTS(2, 13, 1024)
+  HTS(4, 13, 1024)
   vs.push_back({"hillis tile U1", true, [=](hipStream_t s) {
                   return launch_tile_scan<float, double, 1, 4, 1, true, 0>(x, y, nullptr, n, k, s);
                 }});
@@ -320,6 +328,9 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   TILES(4, 4, 512)
   TILES(4, 5, 512)
   TILES(4, 13, 512)
+  TILES(4, 13, 256)
+  TILES(2, 3, 256)
+  TILES(4, 3, 256)
   TILES(4, 1, 512)
   TILES(2, 0, 512)
   TILES(2, 1, 512)
@@ -434,6 +445,16 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
     STILES(2, 0, 1024)
     STILES(2, 5, 1024)
     STILES(2, 13, 1024)
+#define SHTS(U, NT, WG)                                                                                 \
+  vs.push_back({"i16 stereo hillisS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                 \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, true, NT, WG>(x, y, nullptr, n / 2, k, s); \
+                }});
+    SHTS(4, 0, 256)
+    SHTS(4, 3, 256)
+    SHTS(4, 13, 256)
+    SHTS(8, 3, 256)
+    SHTS(8, 13, 256)
+    SHTS(4, 13, 512)
 #define STILEWG(U, WG, RC)                                                                              \
   vs.push_back({"i16 stereo tile U" #U " wg" #WG " rc" #RC, true, [=](hipStream_t s) {                    \
                   return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, 0, WG, RC>(x, y, nullptr, n / 2, k, s, 64); \
@@ -504,6 +525,16 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   ITILES(2, 0, 1024)
   ITILES(2, 5, 1024)
   ITILES(2, 13, 1024)
+#define IHTS(U, NT, WG)                                                                                 \
+  vs.push_back({"i16 hillisS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                        \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, true, NT, WG>(x, y, nullptr, n, k, s); \
+                }});
+  IHTS(4, 0, 256)
+  IHTS(4, 3, 256)
+  IHTS(4, 13, 256)
+  IHTS(8, 3, 256)
+  IHTS(8, 13, 256)
+  IHTS(4, 13, 512)
 #define ITILENR(U, NT)                                                                                  \
   vs.push_back({"i16 tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                             \
                   return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, 256, false>(x, y, nullptr, n, k, s); \
