@@ -8,6 +8,7 @@
 #include <mutex>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 #include "../../include/mavg.h"
 #include "mavg_kernels.hpp"
@@ -42,9 +43,9 @@ template <> constexpr const char* type_name<int32_t>() { return "i32"; }
 template <> constexpr const char* type_name<int64_t>() { return "i64"; }
 
 // family entry points (defined in mavg_scan_*.hip / mavg_direct.hip)
-// Workspace: the look-back scan needs kLookbackHeader + ntiles*C*8 bytes of
-// caller-owned device memory (reset on the stream before each launch); every
-// other launch needs none.
+// Workspace: the look-ahead scan needs its record granules (ahead_granule_bytes)
+// in caller-owned device memory (zeroed on the stream before each launch);
+// every other launch needs none.
 struct Workspace {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -163,48 +164,73 @@ int launch_tile_scan(const void* in, void* out, const void* hist, long long nfra
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
-// look-back tile scan (two launches): pass 1 writes every whole tile's sum
-// into the workspace, pass 2 scans each tile with its carry from those sums
-template <typename T, typename A, int C, int F, int U, int NT = 0>
-int launch_lookback_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
-                         Workspace ws, int xcd_remap = kRemapGroup) {
+// look-ahead scan (one pass over HBM): zero the record granules, then one
+// launch whose tile t publishes the records of tile t + ahead and scans
+// tile t with its carry from earlier records (mavg_lookback.hpp).
+// Workspace: the granule block, at the start of the workspace, padded to
+// 16 bytes (the memset's fast form, cdna_hip_programming.md Guideline 16).
+constexpr int kAheadSlots = 512;  // D: dispatch slots between a record's producer and its tile (multiple of 8)
+constexpr int kAheadSpin = 256;   // polls of an untagged granule before recomputing it
+// Test knobs: MAVG_AHEAD_SLOTS / MAVG_AHEAD_SPIN override the two constants
+// (the parity tests force the recompute path with SPIN=0 and short or absent
+// look-ahead); results are bitwise the same for every setting.
+inline int ahead_knob(const char* name, int dflt, int lo, int hi) {
+  const char* v = getenv(name);
+  if (v == nullptr || *v == 0) return dflt;
+  const long x = strtol(v, nullptr, 10);
+  return (int)std::min<long>(hi, std::max<long>(lo, x));
+}
+template <typename T, typename A, int C, int F, int U>
+constexpr size_t ahead_granule_bytes(long long nfull) {
+  using SA = typename ScanAcc<T, A>::type;
+  // + 16 bytes of launch statistics (MAVG_AHEAD_STATS builds only)
+  return (((size_t)(nfull > 0 ? nfull : 1) * kNW * C * GranCount<SA>::n * 8) + 15) / 16 * 16 + 16;
+}
+template <typename T, typename A, int C, int F, int U, int NT = kNtStore, int ORD = 2, bool RC = false, int WPS = 1>
+int launch_ahead_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
+                      Workspace ws, int ahead = -1, int spin = -1) {
+  if (ahead < 0) ahead = ahead_knob("MAVG_AHEAD_SLOTS", kAheadSlots, 0, 1 << 30) & ~7;
+  if (spin < 0) spin = ahead_knob("MAVG_AHEAD_SPIN", kAheadSpin, 0, 1 << 20);
+  constexpr int xcd_remap = 1;  // one run per XCD (see ahead_scan_kernel)
   constexpr int TF = kWG * F * U;
   constexpr int VE = F * C;
   constexpr int NSEG = U * kNW;
+  using SA = typename ScanAcc<T, A>::type;
   constexpr size_t kStageBytes = (((size_t)(U * kWG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15;
   const long long ntiles = (nframes + TF - 1) / TF;
   const long long nfull = nframes / TF;
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
-  using SA = typename ScanAcc<T, A>::type;  // whole-tile sums
-  const size_t need = (size_t)kLookbackHeader + (size_t)std::max<long long>(nfull, 1) * C * sizeof(SA);
-  const size_t lds = kStageBytes + (size_t)(NSEG + kNW) * C * sizeof(A);
+  const size_t need = ahead_granule_bytes<T, A, C, F, U>(nfull);
+  const size_t lds = kStageBytes + (size_t)kNW * C * sizeof(A) + (size_t)NSEG * C * sizeof(SA);
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "lookback_scan<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d> grid=%lld+%lld block=%d lds=%zu tile_frames=%d "
-             "remap=%d ws=%zu",
-             type_name<T>(), type_name<A>(), C, F, U, NT, nfull, ntiles, kWG, lds, TF, xcd_remap, need);
+             "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
+             "ahead=%d remap=%d ws=%zu",
+             type_name<T>(), type_name<A>(), C, F, U, NT, ntiles, kWG, lds, TF, ahead, xcd_remap, need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
   if (ws.ptr == nullptr || ws.bytes < need) return MAVG_ERR_WORKSPACE;
-  if ((reinterpret_cast<uintptr_t>(ws.ptr) & 7u) != 0) return MAVG_ERR_MISALIGNED;
-  SA* sums = reinterpret_cast<SA*>(static_cast<unsigned char*>(ws.ptr) + kLookbackHeader);
-  if (nfull > 0)
-    hipLaunchKernelGGL((tile_sums_kernel<T, A, C, F, U>), dim3((unsigned)nfull), dim3(kWG), 0, st,
-                       static_cast<const T*>(in), sums, nfull, xcd_remap);
-  LookbackParams p{};
+  if ((reinterpret_cast<uintptr_t>(ws.ptr) & 15u) != 0) return MAVG_ERR_MISALIGNED;
+  if (hipMemsetAsync(ws.ptr, 0, need, st) != hipSuccess) return MAVG_ERR_HIP;
+  AheadParams p{};
   p.in = in;
   p.out = out;
   p.hist = hist;
   p.nframes = nframes;
+  p.nfull = nfull;
   p.k = k;
   p.o = make_out_params(k);
   p.halo_units = (k + F - 1) / F;
   p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
   p.xcd_remap = xcd_remap;
-  p.sums = sums;
-  hipLaunchKernelGGL((lookback_scan_kernel<T, A, C, F, U, NT>), dim3((unsigned)ntiles), dim3(kWG), lds, st, p);
+  p.ahead = ahead;
+  p.head = (int)std::min<long long>((long long)k / TF, nfull);
+  p.spin = spin;
+  p.gran = static_cast<unsigned long long*>(ws.ptr);
+  p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
+  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, ORD, RC, WPS>), dim3((unsigned)ntiles), dim3(kWG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
@@ -238,10 +264,10 @@ bool segment_ring_fits(int k) {
 //     int16  H <= 256: U2 nt | H <= 4 KiB: U4 nt | H <= 8 KiB: U4 ntS |
 //            H <= 16 KiB: U4 x 512 threads ntS | H <= ~47 KiB: U2 x 1024 (80 KiB LDS) ntS
 //     fp32   mono H <= 512: U2 nt rc | H <= 4 KiB: U2 ntS rc | H <= 8 KiB: U2 x 512 ntS rc |
-//            H <= 16 KiB: U4 x 512 ntS rc | H <= ~47 KiB: U2 x 1024 ntS rc
-//     longer windows: the two-pass look-back with nt output stores
-//     longer windows: the segment-streaming scan while its LDS ring holds
-//     the window, then the two-pass look-back scan (needs the workspace)
+//            H <= 16 KiB: U4 x 512 ntS rc
+//     longer windows (fp32 H > 16 KiB, int16 past the 1024-thread tile): the
+//     look-ahead scan, U4, nt output stores (needs the workspace); 0.69-0.73
+//     of peak whatever k (tools/tune/sweep_ahead.sh)
 //   Hillis-Steele flavour: the halo-staged tile while it fits LDS (fp32: U4 nt
 //   for H <= 512 B, else U8 ntS; int16: U4 x 512 threads ntS), then the
 //   segment-streaming scan.
@@ -287,11 +313,10 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
         return launch_tile_scan<T, A, C, F, 2, false, kNtS, 512, true>(in, out, hist, nframes, k, st);
       if (halo_bytes <= 16384 && fits(4, 512))
         return launch_tile_scan<T, A, C, F, 4, false, kNtS, 512, true>(in, out, hist, nframes, k, st);
-      if (fits(2, 1024))
-        return launch_tile_scan<T, A, C, F, 2, false, kNtS, 1024, true>(in, out, hist, nframes, k, st);
+      // fp32 halos past 16 KiB: the look-ahead scan beats the 1024-thread
+      // tile (k=8192: 0.73 vs 0.69; k=12000: 0.71 vs 0.64, sweep_ahead.sh)
     }
-    if (segment_ring_fits<T, A, C, F>(k)) return launch_segment_rule<T, A, C, F, false>(in, out, hist, nframes, k, st);
-    return launch_lookback_scan<T, A, C, F, 2, kNtStore>(in, out, hist, nframes, k, st, ws);
+    return launch_ahead_scan<T, A, C, F, 4, kNtStore>(in, out, hist, nframes, k, st, ws);
   } else {
     // Hillis-Steele: the element-wise log-step scans make a tile's compute
     // long, so bigger tiles (fewer halos and barriers per byte) and the split

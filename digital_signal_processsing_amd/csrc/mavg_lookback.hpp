@@ -1,43 +1,10 @@
-// mavg_lookback.hpp -- the two-pass look-back scan (tile_sums_kernel, lookback_scan_kernel).
+// mavg_lookback.hpp -- the look-ahead scan (ahead_scan_kernel): windows too long for an
+// LDS-staged halo, carry from earlier tiles' sums published inside the launch.
 #pragma once
 
 #include "mavg_device.hpp"
 
 namespace mavg {
-
-// ----------------------------------------------------------------------------
-// look-back tile scan (windows too long for an LDS-staged halo or ring)
-//
-// Two launches.  Pass 1 (tile_sums_kernel) writes the sum of every whole tile
-// of T = 256*F*U frames (read-only streaming, 1/2 of the algorithmic bytes for
-// an fp32 pass).  Pass 2 (lookback_scan_kernel) runs the same flat,
-// XCD-remapped tiles as tile_scan_kernel, but never stages the k-frame halo:
-// the carry W[t0-1] (sum of the k frames before the tile) is
-//   * the pass-1 sums of the whole tiles inside [t0-k, t0), plus
-//   * the part of [t0-k, t0) before the first whole tile, which lies inside
-//     the "shifted tile" [t0-k, t0-k+T) staged in LDS for x[n-k] anyway
-//     (frames before 0 come from the history buffer instead),
-// so LDS is ~2 tiles and the per-sample cost is the same for every k.
-// A single-pass variant (each workgroup publishing its tile sum for later
-// tiles to wait on) measured 0.25-0.37 of HBM peak: the tile just before
-// is still loading when its successor needs its sum, and every agent-scope
-// poll is a trip past the XCD's L2.  Pass 1 + pass 2 measured 0.42-0.51
-// (DESIGN.md "Tuning").
-// ----------------------------------------------------------------------------
-constexpr int kLookbackHeader = 256;  // bytes of the workspace before the tile sums (reserved)
-
-struct LookbackParams {
-  const void* in;
-  void* out;
-  const void* hist;
-  long long nframes;
-  int k;
-  int halo_units;   // ceil(k / F): the stage starts halo_units*F frames before the tile
-  int xk_off;       // (-k*C) mod VE
-  int xcd_remap;    // remap mode (remap_tile)
-  const void* sums; // [nfull][C] whole-tile sums (ScanAcc<T, A>), written by tile_sums_kernel
-  OutParams o;
-};
 
 // Accumulator of the in-tile scan: the prefix of d = x - x[n-k] over one
 // tile telescopes to two sums of at most T samples, |.| <= 2 * T * 32768 <=
@@ -50,13 +17,13 @@ template <> struct ScanAcc<int16_t, int64_t> { using type = int32_t; };
 // U units are loaded before any is stored (one memory round trip, not one per
 // unit), plus one extra unit for the misaligned x[n-k] read.
 template <typename T, int C, int F, int U, int WG, int NT>
-__device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, const T* __restrict__ hist,
-                                                   T* stage, long long h0, long long nframes, int k, int tid) {
+__device__ __forceinline__ void stage_shifted_load(const T* __restrict__ in, const T* __restrict__ hist,
+                                                   Unit<T, F * C> (&h)[U + 1], long long h0, long long nframes,
+                                                   int k, int tid) {
   constexpr int VE = F * C;
   using IO = UnitIO<T, VE>;
   using U_t = Unit<T, VE>;
   const bool fast = h0 >= 0 && h0 + (long long)(U * WG + 1) * F <= nframes;
-  U_t h[U + 1];
   auto guarded = [&](int j) {
     U_t r;
     const long long f = h0 + (long long)j * F;
@@ -76,65 +43,158 @@ __device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, con
     for (int u = 0; u < U; ++u) h[u] = guarded(u * WG + tid);
     if (tid == 0) h[U] = guarded(U * WG);
   }
+}
+template <typename T, int C, int F, int U, int WG>
+__device__ __forceinline__ void stage_shifted_store(T* stage, const Unit<T, F * C> (&h)[U + 1], int tid) {
+  constexpr int VE = F * C;
+  using IO = UnitIO<T, VE>;
 #pragma unroll
   for (int u = 0; u < U; ++u) IO::store(stage + (u * WG + tid) * VE, h[u]);
   if (tid == 0) IO::store(stage + (U * WG) * VE, h[U]);
 }
+// Stage the shifted tile [h0, h0 + (U*WG+1)*F) frames in LDS: every lane's
+// U units are loaded before any is stored (one memory round trip, not one per
+// unit), plus one extra unit for the misaligned x[n-k] read.
+template <typename T, int C, int F, int U, int WG, int NT>
+__device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, const T* __restrict__ hist,
+                                                   T* stage, long long h0, long long nframes, int k, int tid) {
+  Unit<T, F * C> h[U + 1];
+  stage_shifted_load<T, C, F, U, WG, NT>(in, hist, h, h0, nframes, k, tid);
+  stage_shifted_store<T, C, F, U, WG>(stage, h, tid);
+}
 
-// pass 1: the sum of every whole tile (per channel), reduced per lane over
-// its units, then across the wave (DPP scan), then across the waves in order
-template <typename T, typename A, int C, int F, int U>
-__global__ __launch_bounds__(kWG) void tile_sums_kernel(const T* __restrict__ in,
-                                                        typename ScanAcc<T, A>::type* __restrict__ sums,
-                                                        long long nfull, int xcd_remap) {
-  using SA = typename ScanAcc<T, A>::type;  // a whole tile's sum fits the scan accumulator
-  constexpr int NW = kWG / 64;
-  constexpr int VE = F * C;
-  constexpr int TF = kWG * F * U;
-  using IO = UnitIO<T, VE>;
-  __shared__ SA wsum[NW * C];
-  const long long j = remap_tile(blockIdx.x, gridDim.x, xcd_remap);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+// ----------------------------------------------------------------------------
+// look-ahead scan: the look-back scan in ONE pass over HBM (windows too long
+// for an LDS-staged halo)
+//
+// The carry W[t0-1] needs the sums of the whole tiles inside [t0-k, t0).  The
+// two-pass scan streams the signal once more to make them; a one-pass scan in
+// which every tile publishes its own sum for later tiles measured 0.15-0.31 of
+// peak (tools/tune/onepass_experiment.hpp): the tiles a window reaches back to
+// were dispatched only m*8 workgroups earlier (m = k/T), well inside the
+// ~2,000 workgroups in flight, so consumers wait on producers that are still
+// loading.  Here the workgroup of tile t publishes the sums of tile t + D
+// Here the workgroup in dispatch slot b publishes the sums of the tile of
+// slot b + D ("look-ahead") before it scans its own tile:
+//   phase A  every wave loads its share of that tile (default policy, so the
+//            lines stay in the XCD's L2 / the MALL) and publishes its partial
+//            sum as 8-byte {tag, 32-bit payload} granules with agent-scope
+//            (sc1) stores (cdna_hip_programming.md Guideline 16, R2: the data
+//            is the flag, no fences); slots b < D publish their own tiles';
+//   phase B  the tile-scan of lookback_scan_kernel, its whole-tile carry read
+//            from the granules with sc1 loads.  The tiles run in remap mode 1
+//            (one contiguous run per XCD), so slot b + D is on b's XCD and
+//            holds b's tile + D/8: the consumers of a record run >= D slots
+//            after its producer, and a tile's own loads hit the lines phase A
+//            brought into that XCD's L2.  The first tiles of a run need the
+//            records of the previous run's last tiles (dispatched last): the
+//            first k/T slots of each run publish those too ("head duty").
+// HBM traffic is the algorithmic 8 B/sample (fp32) plus the granules; the
+// second read of each tile is served by L2 / MALL.
+//
+// Progress never depends on scheduling: a granule still untagged after a
+// bounded number of polls is recomputed by the waiting wave from the input
+// with the producer's lane mapping and order of operations, so the value --
+// and the output -- is bitwise the same either way, whatever the dispatch
+// order.  The granules are zeroed (hipMemsetAsync) before every launch, so a
+// tag is never stale, also under graph replay (Guideline 16, "Re-initialise
+// every call").  The carry adds the records in a fixed order: deterministic.
+// ----------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) unsigned long long gran_t;  // global, never flat
+constexpr unsigned long long kGranTag = 1ull << 32;                   // tag 1 in the high word (0 = empty)
+
+// granules per record value: a 32-bit payload each
+template <typename SA> struct GranCount { static constexpr int n = sizeof(SA) / 4; };
+
+__device__ __forceinline__ void gran_store(gran_t* g, uint32_t v) {
+  __hip_atomic_store(g, kGranTag | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // one sc1 8-B store
+}
+__device__ __forceinline__ unsigned long long gran_load(const gran_t* g) {
+  return __hip_atomic_load(const_cast<gran_t*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+}
+__device__ __forceinline__ uint32_t gran_word(double v, int h) {
+  return h == 0 ? (uint32_t)__double2loint(v) : (uint32_t)__double2hiint(v);
+}
+__device__ __forceinline__ uint32_t gran_word(int32_t v, int) { return (uint32_t)v; }
+template <typename SA> __device__ __forceinline__ SA gran_value(const uint32_t (&w)[GranCount<SA>::n]);
+template <> __device__ __forceinline__ double gran_value<double>(const uint32_t (&w)[2]) {
+  return __hiloint2double((int)w[1], (int)w[0]);
+}
+template <> __device__ __forceinline__ int32_t gran_value<int32_t>(const uint32_t (&w)[1]) { return (int32_t)w[0]; }
+
+// One wave's share of a tile's sum ("record" of wave slot wv): lane l sums its
+// units u*WG + wv*64 + l over u, frames and channels in order, then one DPP
+// wave scan.  Producers (phase A), tiles t < D (own registers) and the
+// recompute path all run this sequence: bitwise the same value.
+template <typename T, typename SA, int C, int F, int U>
+__device__ __forceinline__ void wave_record(const Unit<T, F * C> (&x)[U], SA (&r)[C]) {
   SA ls[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) ls[c] = (SA)0;
-  if (j < nfull) {  // remap_tile is a bijection on [0, gridDim.x) = [0, nfull)
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const Unit<T, VE> x = IO::template load<true>(in + (j * TF + (long long)(u * kWG + tid) * F) * C);
+  for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int fr = 0; fr < F; ++fr)
+    for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-        for (int c = 0; c < C; ++c) ls[c] += to_acc<SA>(x.e[fr * C + c]);
-    }
-  }
+      for (int c = 0; c < C; ++c) ls[c] += to_acc<SA>(x[u].e[fr * C + c]);
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const SA r = readlane(wave_incl_scan(ls[c]), 63);
-    if (lane == 0) wsum[w * C + c] = r;
-  }
-  __syncthreads();
-  if (tid < C && j < nfull) {
-    SA sm = (SA)0;
+  for (int c = 0; c < C; ++c) r[c] = readlane(wave_incl_scan(ls[c]), 63);
+}
+
+// lanes 0 .. C*NG-1 of the wave each store one granule of record (j, wv)
+template <typename SA, int C, int NW>
+__device__ __forceinline__ void publish_record(gran_t* gran, long long j, int wv, const SA (&r)[C], int lane) {
+  constexpr int NG = GranCount<SA>::n;
+  if (lane < C * NG) {
+    const int c = lane / NG, h = lane - c * NG;
+    SA v = r[0];
 #pragma unroll
-    for (int q = 0; q < NW; ++q) sm += wsum[q * C + tid];
-    sums[j * C + tid] = sm;
+    for (int i = 1; i < C; ++i)
+      if (c == i) v = r[i];
+    gran_store(gran + ((j * NW + wv) * C + c) * NG + h, gran_word(v, h));
   }
 }
 
-// pass 2
-template <typename T, typename A, int C, int F, int U, int NT>
-__global__ __launch_bounds__(kWG) void lookback_scan_kernel(LookbackParams p) {
+// first tile of XCD run x under remap mode 1 (remap_tile)
+__device__ __forceinline__ long long run_start(unsigned x, unsigned nb) {
+  const unsigned q = nb >> 3, r = nb & 7u;
+  return (long long)(x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q);
+}
+
+struct AheadParams {
+  const void* in;
+  void* out;
+  const void* hist;
+  long long nframes;
+  long long nfull;  // whole tiles (the only ones a carry sums)
+  int k;
+  int halo_units;   // ceil(k / F): the stage starts halo_units*F frames before the tile
+  int xk_off;       // (-k*C) mod VE
+  int xcd_remap;    // remap mode (remap_tile)
+  int ahead;        // D (a multiple of 8): block b publishes the records of block b + D's tile
+  int head;         // whole tiles a window can span (k / T): the head duty of remap mode 1
+  int spin;         // polls of an untagged granule before recomputing it
+  unsigned long long* gran;  // [nfull][NW][C][NG] granules, zeroed before the launch
+  void* stats;               // MAVG_AHEAD_STATS builds only: {recomputes, polls that waited}
+  OutParams o;
+};
+
+// ORD: 0 = phase A, then the tile and the stage; 1 = phase A loads, tile
+// loads, phase A record, stage; 2 = tile, stage and phase A loads all in
+// flight, then the stage stores and the phase A record
+template <typename T, typename A, int C, int F, int U, int NT, int ORD = 2, bool RC = false, int WPS = 1>
+__global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   constexpr int WG = kWG;
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
   constexpr int TF = WG * F * U;
   constexpr int NSEG = U * NW;
-  constexpr int kStageUnits = U * WG + 1;  // the shifted tile + one unit for the misaligned x[n-k] read
+  constexpr int kStageUnits = U * WG + 1;
   constexpr int kStageBytes = ((kStageUnits * VE * (int)sizeof(T)) + 15) & ~15;
   using IO = UnitIO<T, VE>;
   using U_t = Unit<T, VE>;
-  using SA = typename ScanAcc<T, A>::type;  // in-tile scan; the carry stays in A
+  using SA = typename ScanAcc<T, A>::type;
+  constexpr int NG = GranCount<SA>::n;
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* stage = reinterpret_cast<T*>(smem);
@@ -144,8 +204,7 @@ __global__ __launch_bounds__(kWG) void lookback_scan_kernel(LookbackParams p) {
   const T* __restrict__ in = static_cast<const T*>(p.in);
   T* __restrict__ out = static_cast<T*>(p.out);
   const T* __restrict__ hist = static_cast<const T*>(p.hist);
-  const typename ScanAcc<T, A>::type* __restrict__ sums =
-      static_cast<const typename ScanAcc<T, A>::type*>(p.sums);
+  gran_t* gran = (gran_t*)p.gran;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = tid >> 6;
@@ -155,70 +214,121 @@ __global__ __launch_bounds__(kWG) void lookback_scan_kernel(LookbackParams p) {
   const long long tile = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
   const long long t0 = tile * TF;
   const int Ha = p.halo_units * F;
-  const long long h0 = t0 - Ha;               // first staged frame (shifted tile, aligned down to F)
+  const long long h0 = t0 - Ha;
   const bool tile_full = (t0 + TF <= nframes);
-  // whole tiles inside the window before t0: [jlo, tile); the rest of the
-  // window, [a, jlo*TF), is read from the stage (a >= 0) or the history
   const long long a = t0 - k;
   const long long jlo = a >= 0 ? (a + TF - 1) / TF : 0;
+  const long long qlo = jlo * NW, qhi = tile * NW;  // records of the whole tiles [jlo, tile)
 
-  // ---- tile -> registers (streamed once) ----
+  // ---- phase A (this wave's share of tile t + D -> record) and phase B's
+  //      loads: the tile (an L2 / MALL hit: phase A of tile t-D) and the
+  //      shifted tile ----
+  const unsigned nb = gridDim.x;
+  const unsigned bd = blockIdx.x + (unsigned)p.ahead;  // the block D dispatch slots later (same XCD)
+  const long long ja = bd < nb ? remap_tile(bd, nb, p.xcd_remap) : -1;
+  const bool produce = ja >= 0 && ja < p.nfull;
+  U_t xa[U];
+  auto load_a = [&]() {
+    if (produce)
+#pragma unroll
+      for (int u = 0; u < U; ++u) xa[u] = IO::load(in + (ja * TF + (long long)(u * WG + tid) * F) * C);
+  };
+  auto publish_a = [&]() {
+    if (produce) {
+      SA r[C];
+      wave_record<T, SA, C, F, U>(xa, r);
+      publish_record<SA, C, NW>(gran, ja, w, r, lane);
+    }
+  };
   U_t x[U];
+  auto load_tile = [&]() {
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const long long f = t0 + (long long)(u * WG + tid) * F;
-    if (tile_full) {
-      x[u] = IO::template load<(NT & kNtLoad) != 0>(in + f * C);
-    } else {
+    for (int u = 0; u < U; ++u) {
+      const long long f = t0 + (long long)(u * WG + tid) * F;
+      if (tile_full) {
+        x[u] = IO::template load<(NT & kNtLoad) != 0>(in + f * C);
+      } else {
 #pragma unroll
-      for (int fr = 0; fr < F; ++fr)
+        for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-        for (int c = 0; c < C; ++c) x[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+          for (int c = 0; c < C; ++c) x[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+      }
+    }
+  };
+  if constexpr (ORD == 0) {
+    load_a();
+    publish_a();
+    load_tile();
+    stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, tid);
+  } else if constexpr (ORD == 1) {
+    load_a();
+    load_tile();
+    publish_a();
+    stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, tid);
+  } else {
+    U_t hs[U + 1];
+    load_tile();
+    stage_shifted_load<T, C, F, U, WG, NT>(in, hist, hs, h0, nframes, k, tid);
+    load_a();
+    stage_shifted_store<T, C, F, U, WG>(stage, hs, tid);
+    publish_a();
+  }
+  if (blockIdx.x < (unsigned)p.ahead && tile < p.nfull) {  // no block D slots earlier: the tile itself
+    SA r[C];
+    wave_record<T, SA, C, F, U>(x, r);
+    publish_record<SA, C, NW>(gran, tile, w, r, lane);
+  }
+  // head duty (remap mode 1): the first tiles of XCD run x need the records of
+  // the last tiles of run x-1, whose blocks are dispatched at the end of the
+  // grid; the first `head` blocks of run x publish those records instead
+  if (p.xcd_remap == 1) {
+    const unsigned xr = blockIdx.x & 7u, s = blockIdx.x >> 3;
+    if (xr >= 1u && s < (unsigned)p.head) {
+      const long long j = run_start(xr, nb) - p.head + s;
+      if (j >= 0 && j < p.nfull) {
+        U_t xh[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) xh[u] = IO::load(in + (j * TF + (long long)(u * WG + tid) * F) * C);
+        SA r[C];
+        wave_record<T, SA, C, F, U>(xh, r);
+        publish_record<SA, C, NW>(gran, j, w, r, lane);
+      }
     }
   }
-  // ---- carry, whole-tile part (loads issued while the tile streams in) ----
-  A hq[C];
+  // first round of record loads (checked after the in-tile scan)
+  unsigned long long rv[C][NG];
+  {
+    const long long q = qlo + tid;
 #pragma unroll
-  for (int c = 0; c < C; ++c) hq[c] = (A)0;
-  for (long long j = jlo + tid; j < tile; j += WG)
+    for (int c = 0; c < C; ++c)
 #pragma unroll
-    for (int c = 0; c < C; ++c) hq[c] += (A)sums[j * C + c];
-  // ---- shifted tile [h0, h0 + kStageUnits*F) -> LDS (read k frames back:
-  //      L2 / MALL) ----
-  stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, tid);
+      for (int h = 0; h < NG; ++h) rv[c][h] = q < qhi ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
+  }
   __syncthreads();
 
-  // ---- carry W[t0-1] = partial + whole tiles ----
-  {
-    A hp[C];
+  // ---- partial carry: the part of [a, t0) before the first whole tile ----
+  A hp[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) hp[c] = (A)0;
-    if (a >= 0) {
-      const int pcount = (int)(jlo * TF - a);  // < TF frames, inside the stage
-      const int s0 = Ha - k;                   // stage frame of a
-      for (int i = tid; i < pcount; i += WG)
+  for (int c = 0; c < C; ++c) hp[c] = (A)0;
+  if (a >= 0) {
+    const int pcount = (int)(jlo * TF - a);
+    const int s0 = Ha - k;
+    for (int i = tid; i < pcount; i += WG)
 #pragma unroll
-        for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(stage[(s0 + i) * C + c]);
-    } else if (hist != nullptr) {
-      // frames [a, 0): the history; only tiles with t0 < k
-      for (long long f = a + tid; f < 0; f += WG)
+      for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(stage[(s0 + i) * C + c]);
+  } else if (hist != nullptr) {
+    for (long long f = a + tid; f < 0; f += WG)
 #pragma unroll
-        for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(load_elem(in, hist, f, c, C, nframes, k));
-    }
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const A r = readlane(wave_incl_scan(hp[c] + hq[c]), 63);
-      if (lane == 0) hsum[w * C + c] = r;
-    }
+      for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(load_elem(in, hist, f, c, C, nframes, k));
   }
 
   // ---- d = x - x[n-k]; in-lane, wave and segment scans ----
-  SA v[U][F][C];
-  SA lx[U][C];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int j = u * WG + tid;
-    const int e = (Ha + j * F - k) * C;      // stage element of x[n-k]
+  // RC: only each lane's total crosses the second barrier; the in-lane
+  // prefix is rebuilt afterwards from x (registers) and the stage, in the
+  // same order, so the outputs are bitwise the same with U*F*C fewer live
+  // accumulators (as in tile_scan_kernel)
+  auto stage_xk = [&](int j) -> U_t {
+    const int e = (Ha + j * F - k) * C;  // stage element of x[n-k]
     U_t xk;
     if constexpr (IO::kVec) {
       if (p.xk_off == 0) {
@@ -233,27 +343,115 @@ __global__ __launch_bounds__(kWG) void lookback_scan_kernel(LookbackParams p) {
 #pragma unroll
       for (int i = 0; i < VE; ++i) xk.e[i] = stage[e + i];
     }
+    return xk;
+  };
+  SA v[RC ? 1 : U][F][C];
+  SA lx[U][C];
 #pragma unroll
-    for (int fr = 0; fr < F; ++fr)
+  for (int u = 0; u < U; ++u) {
+    const U_t xk = stage_xk(u * WG + tid);
+    SA run[C];
+    if constexpr (RC) {
 #pragma unroll
-      for (int c = 0; c < C; ++c) v[u][fr][c] = to_acc<SA>(x[u].e[fr * C + c]) - to_acc<SA>(xk.e[fr * C + c]);
+      for (int c = 0; c < C; ++c) run[c] = (SA)0;
 #pragma unroll
-    for (int fr = 1; fr < F; ++fr)
+      for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-      for (int c = 0; c < C; ++c) v[u][fr][c] += v[u][fr - 1][c];
+        for (int c = 0; c < C; ++c) run[c] += to_acc<SA>(x[u].e[fr * C + c]) - to_acc<SA>(xk.e[fr * C + c]);
+    } else {
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const SA d = to_acc<SA>(x[u].e[fr * C + c]) - to_acc<SA>(xk.e[fr * C + c]);
+          v[u][fr][c] = fr == 0 ? d : v[u][fr - 1][c] + d;
+        }
+#pragma unroll
+      for (int c = 0; c < C; ++c) run[c] = v[u][F - 1][c];
+    }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      const SA t = v[u][F - 1][c];
-      const SA incl = wave_incl_scan(t);
-      lx[u][c] = incl - t;
+      const SA incl = wave_incl_scan(run[c]);
+      lx[u][c] = incl - run[c];
       const SA segtot = readlane(incl, 63);
       if (lane == 0) tot[(u * NW + w) * C + c] = segtot;
     }
   }
+
+  // ---- whole-tile carry from the records (rounds of WG records) ----
+  A hq[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) hq[c] = (A)0;
+  for (long long qb = qlo; qb < qhi; qb += WG) {
+    const long long q = qb + tid;
+    const bool act = q < qhi;
+    if (qb != qlo) {
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int h = 0; h < NG; ++h) rv[c][h] = act ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
+    }
+    for (int it = 0;; ++it) {
+      bool miss = false;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int h = 0; h < NG; ++h) miss |= act && (rv[c][h] >> 32) != 1ull;
+      if (!__any(miss) || it >= p.spin) break;
+#ifdef MAVG_AHEAD_STATS
+      if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats) + 1, 1u);
+#endif
+      __builtin_amdgcn_s_sleep(2);
+      if (miss)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+          for (int h = 0; h < NG; ++h) rv[c][h] = gran_load(gran + (q * C + c) * NG + h);
+    }
+    bool miss = false;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int h = 0; h < NG; ++h) miss |= act && (rv[c][h] >> 32) != 1ull;
+    // still untagged: the wave recomputes each such record from the input
+    unsigned long long mask = __ballot(miss);
+    while (mask != 0ull) {
+      const int l = __builtin_ctzll(mask);
+      mask &= mask - 1ull;
+      const long long qq = __shfl(q, l, 64);
+      const long long jj = qq / NW;
+      const int wv = (int)(qq - jj * NW);
+      U_t xr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) xr[u] = IO::load(in + (jj * TF + (long long)(u * WG + wv * 64 + lane) * F) * C);
+      SA r[C];
+      wave_record<T, SA, C, F, U>(xr, r);
+      if (lane == l)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+          for (int h = 0; h < NG; ++h) rv[c][h] = kGranTag | gran_word(r[c], h);
+#ifdef MAVG_AHEAD_STATS
+      if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats), 1u);
+#endif
+    }
+    if (act)
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        uint32_t wd[NG];
+#pragma unroll
+        for (int h = 0; h < NG; ++h) wd[h] = (uint32_t)rv[c][h];
+        hq[c] += (A)gran_value<SA>(wd);
+      }
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const A r = readlane(wave_incl_scan(hp[c] + hq[c]), 63);
+    if (lane == 0) hsum[w * C + c] = r;
+  }
   __syncthreads();
 
   // ---- carry + earlier segments; outputs ----
-  // segment prefixes by one exclusive wave scan of the totals (mavg_tile.hpp)
   static_assert(NSEG <= 64, "segment totals are scanned across one wave");
   const int wu = __builtin_amdgcn_readfirstlane(w);
   A base[U][C];
@@ -271,10 +469,25 @@ __global__ __launch_bounds__(kWG) void lookback_scan_kernel(LookbackParams p) {
   for (int u = 0; u < U; ++u) {
     const long long f = t0 + (long long)(u * WG + tid) * F;
     U_t y;
+    if constexpr (RC) {
+      const U_t xk = stage_xk(u * WG + tid);
+      SA run[C];
 #pragma unroll
-    for (int fr = 0; fr < F; ++fr)
+      for (int c = 0; c < C; ++c) run[c] = (SA)0;
 #pragma unroll
-      for (int c = 0; c < C; ++c) y.e[fr * C + c] = to_out<T, A>(base[u][c] + (A)(lx[u][c] + v[u][fr][c]), p.o);
+      for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          run[c] += to_acc<SA>(x[u].e[fr * C + c]) - to_acc<SA>(xk.e[fr * C + c]);
+          y.e[fr * C + c] = to_out<T, A>(base[u][c] + (A)(lx[u][c] + run[c]), p.o);
+        }
+    } else {
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          y.e[fr * C + c] = to_out<T, A>(base[u][c] + (A)(lx[u][c] + v[u][fr][c]), p.o);
+    }
     if (tile_full) {
       IO::template store<(NT & kNtStore) != 0>(out + f * C, y);
     } else {

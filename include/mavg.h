@@ -77,11 +77,13 @@ typedef enum {
 } mavg_status;
 
 /* Device workspace (bytes) mavg_run needs for this problem.  0 for every
- * launch except the two-pass look-back scan that AUTO/BLELLOCH pick for
- * windows too long for LDS (e.g. fp32 k > ~12K frames): 256 + one
- * accumulator-sized sum per whole tile and channel (4 MiB for 2^30 fp32
- * samples).  Any alignment of 8 B; contents need no initialisation; one
- * workspace must not serve two launches that may run concurrently. */
+ * launch except the look-ahead scan that AUTO/BLELLOCH pick for windows too
+ * long for an LDS-staged halo (fp32 halos > 16 KiB, e.g. mono k > 4096;
+ * int16 past ~47 KiB): 8 B per (whole tile, wave, channel, 32-bit word of
+ * the tile sum), padded to 16, + 16 (16 MiB for 2^30 fp32 samples).
+ * 16-B alignment; contents need no initialisation (mavg_run zeroes them on
+ * the stream); one workspace must not serve two launches that may run
+ * concurrently. */
 int mavg_workspace_bytes(size_t n_samples, int channels, int grade, int dtype,
                          int algo, int block_size, size_t* out_bytes);
 

@@ -100,38 +100,41 @@ def test_plan_describes_launch_without_gpu():
     assert "nt=13" in p and "nt=13" in dsp.plan(1 << 30, 4096), p
     assert "nt=3" in dsp.plan(1 << 30, 64)  # tiny halo: everything non-temporal
     assert "U=4" in dsp.plan(1 << 30, 4096) and "block=512" in dsp.plan(1 << 30, 4096)
-    assert dsp.plan(1 << 20, 70_000).startswith("lookback_scan<f32")
+    assert dsp.plan(1 << 20, 70_000).startswith("ahead_scan<f32")
     assert dsp.plan(1 << 20, 70_000, algo="hillis").startswith("segment_scan<") and "xkg=1" in dsp.plan(
         1 << 20, 70_000, algo="hillis")
     assert dsp.plan(1 << 20, 7, algo="direct").startswith("direct<f32")
     assert dsp.plan(1 << 20, 7, algo="naive").startswith("naive<f32")
     assert "hillis" in dsp.plan(1 << 20, 7, algo="hillis_scalar")
-    assert dsp.plan(1 << 20, 100_000, dtype=dsp.I16).startswith("lookback_scan<i16,acc=i64")
+    assert dsp.plan(1 << 20, 100_000, dtype=dsp.I16).startswith("ahead_scan<i16,acc=i64")
     assert dsp.plan(3 * 1000, 7, channels=3, dtype=dsp.I16, algo="blelloch").startswith("tile_scan<i16,acc=i32,C=3,F=1")
     with pytest.raises(dsp.MavgError):
         dsp.plan(10, 0)
 
 
-def test_workspace_only_for_lookback():
+def test_workspace_only_for_ahead_scan():
     import digital_signal_processsing_amd as dsp
-    # halo-staged tiles need none; the look-back scan needs a ticket word and
-    # one 8-byte sum per (tile, channel)
+    # halo-staged tiles need none; the look-ahead scan needs its record
+    # granules: 8 bytes per (whole tile, wave, channel, 32-bit word of the
+    # tile-sum type), padded to 16 bytes, plus 16 bytes of statistics
     assert dsp.workspace_bytes(1 << 30, 1024) == 0
     assert dsp.workspace_bytes(1 << 30, 4096) == 0
-    # k=8192 fp32 fits a 1024-thread tile (80 KiB of LDS); k=20000 does not
-    assert dsp.workspace_bytes(1 << 30, 8192) == 0 and "block=1024" in dsp.plan(1 << 30, 8192)
+    # fp32 halos past 16 KiB take the look-ahead scan (U=4: 4096-frame tiles)
+    tiles = (1 << 30) // 4096
+    assert dsp.plan(1 << 30, 8192).startswith("ahead_scan<f32,acc=f64,C=1,F=4,U=4")
+    assert dsp.workspace_bytes(1 << 30, 8192) == tiles * 4 * 2 * 8 + 16
+    assert "ws=%d" % (tiles * 4 * 2 * 8 + 16) in dsp.plan(1 << 30, 20_000)
     assert dsp.plan(1 << 30, 8192, algo="hillis").startswith("segment_scan<")
-    tiles = (1 << 30) // 2048  # whole tiles: one fp64 sum each
-    assert dsp.workspace_bytes(1 << 30, 20_000) == 256 + tiles * 8
-    assert "ws=%d" % (256 + tiles * 8) in dsp.plan(1 << 30, 20_000)
+    # int16 keeps the 1024-thread tile up to ~47 KiB of halo
+    assert dsp.workspace_bytes(1 << 30, 8192, dtype=dsp.I16) == 0
     n = 2 * 1_000_003
-    st = (n // 2) // 2048     # int16 stereo: one int32 sum per (whole tile, channel)
-    assert dsp.workspace_bytes(n, 44100, 2, dsp.I16) == 256 + st * 2 * 4
+    st = (n // 2) // 4096     # int16 stereo: one int32 word per (whole tile, wave, channel)
+    assert dsp.workspace_bytes(n, 44100, 2, dsp.I16) == (st * 4 * 2 * 8 + 15) // 16 * 16 + 16
     assert dsp.workspace_bytes(1 << 20, 70_000, algo="hillis") == 0
     assert dsp.workspace_bytes(0, 70_000) == 0
 
 
-def test_lookback_without_workspace_is_an_error():
+def test_ahead_scan_without_workspace_is_an_error():
     lib = _lib.load()
     # plan mode is not used here: a real call with dummy aligned pointers must
     # refuse before touching the device when the workspace is missing

@@ -281,16 +281,17 @@ def test_many_channels_auto(oracle_mod, gpu):
 
 
 # ---------------------------------------------------------------------------
-# look-back tile scan (long windows): carry from the pass-1 tile sums
+# look-ahead scan (long windows): carry from whole-tile records published
+# inside the launch (mavg_lookback.hpp)
 def _lookback_tile(dsp, n, k, C, dt):
     plan = dsp.plan(n, k, C, dt)
-    assert plan.startswith("lookback_scan<"), plan
+    assert plan.startswith("ahead_scan<"), plan
     return int(plan.split("tile_frames=")[1].split()[0])
 
 
 @pytest.mark.parametrize("C", [1, 2, 3, 8])
 @pytest.mark.parametrize("dtype", ["i16", "f32"])
-def test_lookback_window_edges(oracle_mod, gpu, C, dtype):
+def test_ahead_window_edges(oracle_mod, gpu, C, dtype):
     """k just below / at / above multiples of the tile (empty, one-frame and
     full partial pieces), windows spanning many tiles, int16 k > 65535, and a
     ragged tail tile."""
@@ -299,7 +300,7 @@ def test_lookback_window_edges(oracle_mod, gpu, C, dtype):
     frames = 200_003
     T = _lookback_tile(dsp, frames * C, 70_001, C, dt)
     for k in sorted({16 * T - 1, 16 * T, 16 * T + 1, 20_000, 44_100, 70_001}):
-        if dsp.plan(frames * C, k, C, dt).split("<")[0] != "lookback_scan":
+        if dsp.plan(frames * C, k, C, dt).split("<")[0] != "ahead_scan":
             continue
         if dtype == "i16":
             x = oracle_mod.synth_i16(frames * C, offset=k + C)
@@ -310,7 +311,7 @@ def test_lookback_window_edges(oracle_mod, gpu, C, dtype):
 
 
 @pytest.mark.parametrize("frames", [1, 777, 44_099, 44_100, 44_101, 100_000])
-def test_lookback_short_signals(oracle_mod, gpu, frames):
+def test_ahead_short_signals(oracle_mod, gpu, frames):
     """Signals shorter than (or about as long as) the window: every tile's
     window reaches before frame 0."""
     k, C = 44_100, 2
@@ -322,7 +323,7 @@ def test_lookback_short_signals(oracle_mod, gpu, frames):
 
 @pytest.mark.parametrize("dtype", ["i16", "f32"])
 @pytest.mark.parametrize("cut", [5_000, 37_001])
-def test_lookback_history_equals_concatenation(oracle_mod, gpu, dtype, cut):
+def test_ahead_history_equals_concatenation(oracle_mod, gpu, dtype, cut):
     """History with a long window: the part of the window before frame 0 comes
     from the history buffer (cut < k: the window also reaches before it)."""
     C, k, frames = 2, 20_000, 120_000
@@ -357,8 +358,8 @@ def test_int64_division_edges(oracle_mod, gpu):
 
 
 @pytest.mark.parametrize("own_workspace", [True, False])
-def test_lookback_graph_capture(oracle_mod, gpu, own_workspace):
-    """The workspace reset and the look-back launch replay correctly from a
+def test_ahead_graph_capture(oracle_mod, gpu, own_workspace):
+    """The granule reset and the look-ahead launch replay correctly from a
     captured HIP graph, repeatedly, with a caller-owned workspace; without one
     the binding refuses inside a capture (no workspace from the capture's
     private pool, which is freed again before the capture ends)."""
@@ -367,7 +368,7 @@ def test_lookback_graph_capture(oracle_mod, gpu, own_workspace):
     n, k = 1_000_003, 30_000
     x = torch.from_numpy(oracle_mod.synth_f32(n, seed=23, dist=1)).to(gpu)
     y = torch.empty_like(x)
-    assert dsp.plan(n, k).startswith("lookback_scan<")
+    assert dsp.plan(n, k).startswith("ahead_scan<")
     ws = torch.empty(dsp.workspace_bytes(n, k), dtype=torch.uint8, device=gpu) if own_workspace else None
     s = torch.cuda.Stream(device=gpu)
     s.wait_stream(torch.cuda.current_stream(gpu))
@@ -392,7 +393,7 @@ def test_lookback_graph_capture(oracle_mod, gpu, own_workspace):
         assert_f32_close(y.cpu().numpy(), ref, f"replay {i}")
 
 
-def test_lookback_large_stereo_slices(oracle_mod, gpu):
+def test_ahead_large_stereo_slices(oracle_mod, gpu):
     """2^27 int16 stereo samples, one-second window at 44.1 kHz (k=44100):
     bit-exact at random slices, the first tiles and the tail."""
     import digital_signal_processsing_amd as dsp
@@ -414,9 +415,84 @@ def test_lookback_large_stereo_slices(oracle_mod, gpu):
         assert np.array_equal(y[s * C:(s + span) * C], ref), f"slice at frame {s}"
 
 
+def _with_env(env, fn):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    try:
+        os.environ.update({k: str(v) for k, v in env.items()})
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("dtype,C,k", [("f32", 1, 20_000), ("f32", 3, 9_000), ("i16", 2, 44_100),
+                                       ("i16", 1, 100_000)])
+def test_ahead_records_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, k):
+    """Every record is the same bits whether its producer published it (look-
+    ahead D slots, head duty, own tile) or the consumer recomputed it after a
+    bounded wait: forcing the recompute path (SPIN=0), the one-pass form
+    (SLOTS=0: every tile publishes only its own records), minimal and absent
+    look-ahead gives bitwise the same output as the default schedule, also for
+    fp32 data whose sums round (uniform [0,1) values), and it matches the
+    oracle.  Signal lengths give ragged XCD runs (tiles not a multiple of 8)."""
+    import digital_signal_processsing_amd as dsp
+    dt = dsp.F32 if dtype == "f32" else dsp.I16
+    frames = 2_600_000 // C + 12_345  # > D = 512 tiles at C=1: the look-ahead producers run
+    assert dsp.plan(frames * C, k, C, dt).startswith("ahead_scan<")
+    if dtype == "f32":
+        x = oracle_mod.synth_f32(frames * C, seed=77, dist=1)
+    else:
+        x = oracle_mod.synth_i16(frames * C, seed=77)
+    base = _run(x, k, C, "auto", gpu)
+    for env in ({"MAVG_AHEAD_SPIN": 0}, {"MAVG_AHEAD_SLOTS": 0}, {"MAVG_AHEAD_SLOTS": 8},
+                {"MAVG_AHEAD_SLOTS": 1 << 28}, {"MAVG_AHEAD_SLOTS": 8, "MAVG_AHEAD_SPIN": 0}):
+        y = _with_env(env, lambda: _run(x, k, C, "auto", gpu))
+        assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), env
+    if dtype == "f32":
+        assert_f32_close(base, oracle_mod.mavg_f32(x, k, C), f"C={C} k={k}")
+    else:
+        assert np.array_equal(base, oracle_mod.mavg_i16(x, k, C))
+
+
+@pytest.mark.parametrize("fill", [0xFF, "tags"])
+def test_ahead_poisoned_workspace(oracle_mod, gpu, fill):
+    """The granules are zeroed on the stream before every launch: a caller
+    workspace holding garbage -- including words that look like valid tagged
+    records -- does not leak into the carry."""
+    import digital_signal_processsing_amd as dsp
+    import torch
+    n, k = 600_001, 33_333
+    x = torch.from_numpy(oracle_mod.synth_f32(n, seed=5, dist=1)).to(gpu)
+    y = torch.empty_like(x)
+    nb = dsp.workspace_bytes(n, k)
+    assert nb > 0
+    if fill == 0xFF:
+        ws = torch.full((nb,), 0xFF, dtype=torch.uint8, device=gpu)
+    else:  # every 8-byte word = {tag 1, payload 0x3ff00000}: a plausible record
+        ws = torch.full((nb // 8,), (1 << 32) | 0x3FF00000, dtype=torch.int64, device=gpu)
+    dsp.moving_average_into(x, y, k, workspace=ws)
+    assert_f32_close(y.cpu().numpy(), oracle_mod.mavg_f32(oracle_mod.synth_f32(n, seed=5, dist=1), k, 1), str(fill))
+
+
+def test_ahead_deterministic_repeats(oracle_mod, gpu):
+    """Repeated launches of the look-ahead scan on fp32 data whose sums round:
+    bitwise identical outputs (records are summed in a fixed order)."""
+    import digital_signal_processsing_amd as dsp
+    import torch
+    n, k = 1 << 24, 50_000
+    x = dsp.fill_synthetic(n, torch.float32, seed=9, dist=1, device=gpu)
+    y0 = dsp.moving_average(x, k)
+    for _ in range(5):
+        assert torch.equal(dsp.moving_average(x, k).view(torch.int32), y0.view(torch.int32))
+
+
 # ---------------------------------------------------------------------------
 # dispatch boundaries: windows one frame either side of every halo-size
-# threshold of dispatch_scan_f (tile shapes, tile -> segment -> look-back)
+# threshold of dispatch_scan_f (tile shapes, tile -> look-ahead scan)
 def _boundary_windows(dsp, n, C, dt):
     """Every window where the plan (kernel, tile, workgroup) changes, found by
     bisection on mavg_plan (no GPU), as k-1, k, k+1."""
@@ -465,4 +541,4 @@ def test_dispatch_boundaries(oracle_mod, gpu, C, dtype):
             assert np.array_equal(y, ref), (k, frames, use_hist, plan)
         else:
             assert_f32_close(y, ref, f"k={k} frames={frames} hist={use_hist} {plan}")
-    assert len(seen) >= 2, seen  # the sweep crosses kernel shapes (fp32 C=8: tile, look-back)
+    assert len(seen) >= 2, seen  # the sweep crosses kernel shapes (fp32 C=8: tile, look-ahead)

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../digital_signal_processsing_amd/csrc/mavg_launch.hpp"
+#include "twopass_experiment.hpp"
 #include "onepass_experiment.hpp"
 
 using namespace mavg;
@@ -162,6 +163,15 @@ int run(int lg, int k, int rounds) {
       CK(hipMemcpyAsync(&v.mism, dcnt, 8, hipMemcpyDeviceToHost, st));
     }
     CK(hipStreamSynchronize(st));
+    if (v.name.find("ahead") != std::string::npos) {
+      LaunchPlan lp{};
+      g_plan = &lp;
+      v.launch(st);
+      g_plan = nullptr;
+      unsigned int stt[2] = {0, 0};
+      CK(hipMemcpy(stt, static_cast<unsigned char*>(g_ws.ptr) + lp.ws_bytes - 16, 8, hipMemcpyDeviceToHost));
+      printf("%s: recomputes = %u, waiting polls = %u\n", v.name.c_str(), stt[0], stt[1]);
+    }
     if (v.name.find("onepass") != std::string::npos) {
       unsigned int fb = 0;
       CK(hipMemcpy(&fb, g_ws.ptr, 4, hipMemcpyDeviceToHost));
@@ -304,6 +314,17 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   LB(1)
   LB(2)
   LB(4)
+#define AH(U, NT, D, ORD, WPS)                                                                          \
+  vs.push_back({"ahead U" #U " nt" #NT " D" #D " o" #ORD " w" #WPS, true, [=](hipStream_t s) {            \
+                  return launch_ahead_scan<float, double, 1, 4, U, NT, ORD, false, WPS>(x, y, nullptr, n, k, s, g_ws, D); \
+                }});
+  AH(4, 1, 512, 2, 1)
+  AH(4, 1, 512, 2, 5)
+  AH(4, 1, 512, 2, 6)
+  AH(4, 1, 512, 2, 8)
+  AH(4, 1, 512, 1, 6)
+  AH(4, 1, 512, 0, 6)
+  AH(2, 1, 1024, 2, 8)
 #define OP(U, NT)                                                                                       \
   vs.push_back({"onepass U" #U " NT" #NT, true, [=](hipStream_t s) {                                      \
                   return launch_onepass_scan<float, double, 1, 4, U, NT>(x, y, nullptr, n, k, s, g_ws);        \
@@ -423,6 +444,13 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
     SLB(1)
     SLB(2)
     SLB(4)
+#define SAH(U, D, W)                                                                                    \
+  vs.push_back({"i16 stereo ahead U" #U " D" #D " w" #W, true, [=](hipStream_t s) {                       \
+                  return launch_ahead_scan<int16_t, int32_t, 2, 4, U, 1, 2, false, W>(x, y, nullptr, n / 2, k, s, g_ws, D); \
+                }});
+    SAH(4, 512, 1)
+    SAH(4, 512, 6)
+    SAH(4, 512, 8)
 #define SOP(U)                                                                                          \
   vs.push_back({"i16 stereo onepass U" #U, true, [=](hipStream_t s) {                                     \
                   return launch_onepass_scan<int16_t, int32_t, 2, 4, U, 0>(x, y, nullptr, n / 2, k, s, g_ws); \
@@ -503,6 +531,13 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   ILB(1)
   ILB(2)
   ILB(4)
+#define IAH(U, D, W)                                                                                    \
+  vs.push_back({"i16 ahead U" #U " D" #D " w" #W, true, [=](hipStream_t s) {                              \
+                  return launch_ahead_scan<int16_t, int32_t, 1, 8, U, 1, 2, false, W>(x, y, nullptr, n, k, s, g_ws, D); \
+                }});
+  IAH(4, 512, 1)
+  IAH(4, 512, 6)
+  IAH(4, 512, 8)
 #define IOP(U)                                                                                          \
   vs.push_back({"i16 onepass U" #U, true, [=](hipStream_t s) {                                            \
                   return launch_onepass_scan<int16_t, int32_t, 1, 8, U, 0>(x, y, nullptr, n, k, s, g_ws);      \
