@@ -42,6 +42,9 @@ WORKLOADS = {
     "i16_2p30": (1 << 30, 1024, 1, "i16", "blelloch"),
     "i16_stereo_2p30": (1 << 30, 1024, 2, "i16", "blelloch"),
     "hillis_2p30": (1 << 30, 1024, 1, "f32", "hillis"),
+    # a one-second window at 44.1 kHz: too long for an LDS-staged halo, so the
+    # one-pass look-ahead scan (the inter-block carry path beyond config #4)
+    "long_2p30": (1 << 30, 44100, 1, "f32", "blelloch"),
 }
 
 

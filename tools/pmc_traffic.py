@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 
 TYPE = {"f32": "float", "f64": "double", "i16": "short", "i32": "int", "i64": "long"}
 FAMILY = {"tile_scan": "tile_scan_kernel", "segment_scan": "scan_kernel", "direct": "direct_kernel",
-          "naive": "naive_kernel"}
+          "naive": "naive_kernel", "ahead_scan": "ahead_scan_kernel"}
 
 
 def kernel_key(name):
@@ -53,6 +53,8 @@ def plan_key(plan):
         args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["nt"], wg, "true" if kv.get("rc", "1") == "1" else "false")
     elif fam == "direct":
         args = (T, acc, kv["C"], kv["F"], kv["U"], wg)
+    elif fam == "ahead_scan":  # ORD=2, RC=false, WPS=1: the only instantiation the dispatch makes
+        args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], "2", "false", "1")
     elif fam == "segment_scan":
         args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["pd"], kv["nt"])
     else:
