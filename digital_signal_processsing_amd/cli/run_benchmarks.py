@@ -14,7 +14,15 @@ restricted from the command line (--quick, --sizes, --grades, --blocks,
 --bins), and --verify checks every GPU binary's filtered output against
 bin_cpu's on the same WAV (all variants are bit-exact on int16).
 
+--baseline-configs runs the five BASELINE.json configurations instead of the
+WAV sweep: #1-#4 through the bin_* programs' synthetic fp32
+mode (HBM-resident input, kernel-only timing, roofline line), #5 -- the
+sharded signal, 2^30 samples per GPU, k=1024, (k-1)-sample RCCL halo --
+through bench.py under torch.distributed.run at 1, 2, 4 and 8 GPUs, as many
+as the node has.
+
     cd digital_signal_processsing_amd/cli && python run_benchmarks.py --quick
+    python run_benchmarks.py --baseline-configs --verify
 """
 from __future__ import annotations
 
@@ -43,6 +51,17 @@ BLOCK_SIZES = [32, 64, 128, 256, 512, 1024]
 GRADES = list(range(1, 11)) + list(range(11, 51, 5)) + list(range(50, 1001, 50))
 INPUT_SIZES = [int(v) for v in np.linspace(5000, 50_000_000, 100)]
 TEMP_WAV = "temp_bench.wav"
+REPO = os.path.dirname(os.path.dirname(HERE))
+
+# BASELINE.json configs[0..3]: (label, binary, fp32 samples, grade)
+BASELINE_CONFIGS = {
+    1: ("CPU serial, N=2^20 fp32, k=32", "./bin_cpu", 1 << 20, 32),
+    2: ("Blelloch scan, N=2^26 fp32, k=64, float4 loads", "./bin_vblelloch", 1 << 26, 64),
+    3: ("small-window direct LDS-tiled, N=2^28 fp32, k=7", "./bin_vec4", 1 << 28, 7),
+    4: ("large-window scan, N=2^30 fp32, k=4096", "./bin_vblelloch", 1 << 30, 4096),
+}
+# configs[4]: sharded 2^30 fp32 samples per GPU, k=1024, RCCL halo
+SHARDED_GPUS = (1, 2, 4, 8)
 
 
 def write_wav(path: str, data: np.ndarray, rate: int = 44100) -> None:
@@ -144,6 +163,83 @@ def run_suite(sizes, grades, blocks, bins, verify=False, timeout=600) -> int:
     return failures + mismatches
 
 
+def _field(text: str, key: str):
+    for line in text.splitlines():
+        if line.strip().startswith(key):
+            return line.split(":", 1)[1].strip()
+    return None
+
+
+def _gpu_count() -> int:
+    # a child process counts the devices (torch.cuda.device_count() does not
+    # initialise the GPU on this image); the harness itself stays torch-free
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, universal_newlines=True)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+def run_baseline_configs(configs, verify=False, max_gpus=None, timeout=900) -> int:
+    """The five BASELINE.json configurations; returns the failure count."""
+    import json
+
+    failures = 0
+    rows = []
+    for c in sorted(x for x in configs if x in BASELINE_CONFIGS):
+        label, exe, n, grade = BASELINE_CONFIGS[c]
+        cmd = [exe, "-", str(grade), "256", "--synthetic", str(n), "--dtype", "f32"]
+        if verify:
+            cmd.append("--verify")
+        print(f"== config #{c}: {label}\n   {' '.join(cmd)}", flush=True)
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, universal_newlines=True,
+                           timeout=timeout)
+        print(r.stdout, end="")
+        if r.returncode != 0:
+            failures += 1
+            print(f"Failure: config #{c} rc={r.returncode}\n{r.stderr}")
+            continue
+        if exe == "./bin_cpu":
+            ms = float(_field(r.stdout, "Kernel Compute").split()[0])
+            rows.append((c, label, n / (ms * 1e-3) / 1e9, None, _field(r.stdout, "VERIFY")))
+        else:
+            rows.append((c, label, float(_field(r.stdout, "Gsamples/s")), float(_field(r.stdout, "of 8 TB/s peak")),
+                         _field(r.stdout, "VERIFY")))
+    if 5 in configs:
+        have = _gpu_count() if max_gpus is None else max_gpus
+        for g in [g for g in SHARDED_GPUS if g <= have]:
+            bench = [os.path.join(REPO, "bench.py"), "--gpus", str(g), "--steps", "20", "--warmup", "5",
+                     "--no-cpu-baseline"] + (["--check"] if verify else [])
+            if g == 1:
+                cmd = [sys.executable] + bench
+            else:
+                cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={g}",
+                       "--master-addr", "127.0.0.1", "--master-port", str(29600 + g)] + bench
+            label = f"sharded signal, {g} x 2^30 fp32, k=1024, RCCL halo"
+            print(f"== config #5 ({g} GPU): {' '.join(cmd)}", flush=True)
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, universal_newlines=True,
+                               timeout=timeout, cwd=REPO)
+            lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            if r.returncode != 0 or not lines:
+                failures += 1
+                print(f"Failure: config #5 at {g} GPUs rc={r.returncode}\n{r.stderr[-2000:]}")
+                continue
+            d = json.loads(lines[-1])
+            chk = d.get("check")
+            rows.append((5, label, d["value"], d["roofline"]["frac"] * 1.0,
+                         None if chk is None else f"{chk['mismatches']} mismatches in {chk['slices']} slices"))
+    print("\n__________________________________")
+    print("BASELINE CONFIGS (Gsamples/s; fraction of 8 TB/s per GPU)")
+    for c, label, gs, frac, ver in rows:
+        f = "" if frac is None else f"  {frac:.3f} of HBM peak"
+        v = "" if ver is None else f"  [verify: {ver}]"
+        print(f"#{c} {label}: {gs:.3f} Gsamples/s{f}{v}")
+    print(f"Failures: {failures}")
+    print("__________________________________\n")
+    return failures
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--quick", action="store_true", help="3 sizes x 5 grades x 2 block sizes")
@@ -152,7 +248,13 @@ def main(argv=None) -> int:
     ap.add_argument("--blocks", type=int, nargs="*")
     ap.add_argument("--bins", nargs="*", help="subset, e.g. bin_cpu bin_vblelloch")
     ap.add_argument("--verify", action="store_true", help="compare every GPU binary's output with bin_cpu's")
+    ap.add_argument("--baseline-configs", type=int, nargs="*", metavar="N",
+                    help="run BASELINE.json configs (default all: 1 2 3 4 5) instead of the WAV sweep")
+    ap.add_argument("--max-gpus", type=int, default=None, help="config #5: use at most this many GPUs")
     a = ap.parse_args(argv)
+    if a.baseline_configs is not None:
+        os.chdir(HERE)
+        return 1 if run_baseline_configs(a.baseline_configs or [1, 2, 3, 4, 5], a.verify, a.max_gpus) else 0
     sizes, grades, blocks = INPUT_SIZES, GRADES, BLOCK_SIZES
     if a.quick:
         sizes, grades, blocks = [5000, 1_000_000, 4_000_000], [1, 7, 41, 64, 1000], [64, 256]

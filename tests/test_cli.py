@@ -132,6 +132,44 @@ def test_harness_sweep_tables_match_reference():
     assert len(rb.INPUT_SIZES) == 100 and rb.INPUT_SIZES[0] == 5000 and rb.INPUT_SIZES[-1] == 50_000_000
 
 
+@pytest.mark.parametrize("dtype,C,k", [("f32", 1, 32), ("i16", 2, 5), ("f32", 3, 1000)])
+def test_bin_cpu_synthetic_matches_oracle(tmp_path, oracle_mod, dtype, C, k):
+    """Synthetic north-star mode of bin_cpu (BASELINE config #1 at C=1, k=32):
+    the counter-based signal regenerated on the host, filtered by the serial
+    loop, equals the oracle on the oracle's own generator output."""
+    n = (1 << 16) // C * C
+    r = _run("bin_cpu", "-", k, 256, "--synthetic", n, "--dtype", dtype, "--channels", C, "--verify",
+             "--out", tmp_path / "y.raw", cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "VERIFY: 0 mismatches" in r.stdout
+    if dtype == "f32":
+        x = oracle_mod.synth_f32(n)
+        want = oracle_mod.mavg_f32(x, k, C)
+        got = np.fromfile(tmp_path / "y.raw", dtype=np.float32)
+    else:
+        x = oracle_mod.synth_i16(n)
+        want = oracle_mod.mavg_i16(x, k, C)
+        got = np.fromfile(tmp_path / "y.raw", dtype=np.int16)
+    assert np.array_equal(got, want)
+    rows = list(csv.reader(open(tmp_path / "benchmark_data.csv")))
+    assert rows[1][:5] == ["SingleThreadCpu", "RAM", str(n), str(k), "0"]
+
+
+@pytest.mark.parametrize("args", [["--synthetic", "0"], ["--synthetic", "10", "--dtype", "f64"],
+                                  ["--synthetic", "10", "--channels", "0"], ["--verify"],
+                                  ["--synthetic", "2", "--channels", "3"]])
+def test_synthetic_option_validation(tmp_path, args):
+    r = _run("bin_vblelloch", "-", 4, 256, *args, cwd=tmp_path)
+    assert r.returncode == 1, r.stdout + r.stderr
+
+
+def test_harness_baseline_configs_table():
+    assert {c: (b, n, g) for c, (_, b, n, g) in rb.BASELINE_CONFIGS.items()} == {
+        1: ("./bin_cpu", 1 << 20, 32), 2: ("./bin_vblelloch", 1 << 26, 64), 3: ("./bin_vec4", 1 << 28, 7),
+        4: ("./bin_vblelloch", 1 << 30, 4096)}
+    assert rb.SHARDED_GPUS == (1, 2, 4, 8)
+
+
 # ----------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", GPU_BINS)
@@ -173,3 +211,41 @@ def test_gpu_bins_long_windows(tmp_path, oracle_mod, name):
         assert r.returncode == 0, r.stdout + r.stderr
         y = rb.read_wav_samples(str(tmp_path / "o.wav"))
         assert np.array_equal(y, oracle_mod.mavg_i16(data.reshape(-1), grade, 2)), (name, grade)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,dtype,C,k", [("bin_vblelloch", "f32", 1, 64), ("bin_vec4", "f32", 1, 7),
+                                            ("bin_vhillis", "f32", 2, 1000), ("bin_blelloch", "i16", 2, 44100),
+                                            ("bin_parallel", "i16", 1, 9)])
+def test_gpu_bins_synthetic_match_oracle(tmp_path, oracle_mod, name, dtype, C, k):
+    """Synthetic mode on the device: mavg_fill_synthetic + the variant's kernel
+    against the oracle (int16 bit-exact, fp32 within 1e-5 relative)."""
+    n = 300_007 // C * C
+    r = _run(name, "-", k, 256, "--synthetic", n, "--dtype", dtype, "--channels", C, "--verify",
+             "--out", tmp_path / "y.raw", cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "4. ROOFLINE" in r.stdout and " 0 mismatches" in r.stdout
+    if dtype == "f32":
+        want = oracle_mod.mavg_f32(oracle_mod.synth_f32(n), k, C)
+        got = np.fromfile(tmp_path / "y.raw", dtype=np.float32)
+        np.testing.assert_allclose(got, want, rtol=1e-5, atol=0)  # north_star: 1e-5 relative
+    else:
+        want = oracle_mod.mavg_i16(oracle_mod.synth_i16(n), k, C)
+        assert np.array_equal(np.fromfile(tmp_path / "y.raw", dtype=np.int16), want)
+    rows = list(csv.reader(open(tmp_path / "benchmark_data.csv")))
+    assert rows[1][:3] == [CSV_NAMES[name], "Device", str(n)]
+
+
+@pytest.mark.gpu
+def test_harness_baseline_configs_verify():
+    """The five BASELINE.json configurations through the harness: #1-#4 on the
+    bin_* synthetic mode with span verification, #5 through bench.py --check on
+    the GPUs present (one on the test box)."""
+    r = subprocess.run([sys.executable, os.path.join(CLI, "run_benchmarks.py"), "--baseline-configs", "--verify",
+                        "--max-gpus", "1"],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, universal_newlines=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert "Failures: 0" in r.stdout
+    for c in (1, 2, 3, 4, 5):
+        assert f"\n#{c} " in r.stdout
+    assert r.stdout.count("0 mismatches") >= 5

@@ -319,12 +319,8 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
                   return launch_ahead_scan<float, double, 1, 4, U, NT, ORD, false, WPS>(x, y, nullptr, n, k, s, g_ws, D); \
                 }});
   AH(4, 1, 512, 2, 1)
-  AH(4, 1, 512, 2, 5)
-  AH(4, 1, 512, 2, 6)
-  AH(4, 1, 512, 2, 8)
-  AH(4, 1, 512, 1, 6)
-  AH(4, 1, 512, 0, 6)
-  AH(2, 1, 1024, 2, 8)
+  AH(8, 1, 512, 2, 1)
+  AH(2, 1, 1024, 2, 1)
 #define OP(U, NT)                                                                                       \
   vs.push_back({"onepass U" #U " NT" #NT, true, [=](hipStream_t s) {                                      \
                   return launch_onepass_scan<float, double, 1, 4, U, NT>(x, y, nullptr, n, k, s, g_ws);        \
@@ -444,13 +440,13 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
     SLB(1)
     SLB(2)
     SLB(4)
-#define SAH(U, D, W)                                                                                    \
-  vs.push_back({"i16 stereo ahead U" #U " D" #D " w" #W, true, [=](hipStream_t s) {                       \
-                  return launch_ahead_scan<int16_t, int32_t, 2, 4, U, 1, 2, false, W>(x, y, nullptr, n / 2, k, s, g_ws, D); \
+#define SAH(U, D, W, ORD)                                                                               \
+  vs.push_back({"i16 stereo ahead U" #U " D" #D " w" #W " o" #ORD, true, [=](hipStream_t s) {             \
+                  return launch_ahead_scan<int16_t, int32_t, 2, 4, U, 1, ORD, false, W>(x, y, nullptr, n / 2, k, s, g_ws, D); \
                 }});
-    SAH(4, 512, 1)
-    SAH(4, 512, 6)
-    SAH(4, 512, 8)
+    SAH(4, 512, 1, 2)
+    SAH(2, 1024, 1, 2)
+    SAH(8, 512, 1, 2)
 #define SOP(U)                                                                                          \
   vs.push_back({"i16 stereo onepass U" #U, true, [=](hipStream_t s) {                                     \
                   return launch_onepass_scan<int16_t, int32_t, 2, 4, U, 0>(x, y, nullptr, n / 2, k, s, g_ws); \
@@ -531,13 +527,13 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   ILB(1)
   ILB(2)
   ILB(4)
-#define IAH(U, D, W)                                                                                    \
-  vs.push_back({"i16 ahead U" #U " D" #D " w" #W, true, [=](hipStream_t s) {                              \
-                  return launch_ahead_scan<int16_t, int32_t, 1, 8, U, 1, 2, false, W>(x, y, nullptr, n, k, s, g_ws, D); \
+#define IAH(U, D, W, ORD)                                                                               \
+  vs.push_back({"i16 ahead U" #U " D" #D " w" #W " o" #ORD, true, [=](hipStream_t s) {                    \
+                  return launch_ahead_scan<int16_t, int32_t, 1, 8, U, 1, ORD, false, W>(x, y, nullptr, n, k, s, g_ws, D); \
                 }});
-  IAH(4, 512, 1)
-  IAH(4, 512, 6)
-  IAH(4, 512, 8)
+  IAH(4, 512, 1, 2)
+  IAH(2, 1024, 1, 2)
+  IAH(8, 512, 1, 2)
 #define IOP(U)                                                                                          \
   vs.push_back({"i16 onepass U" #U, true, [=](hipStream_t s) {                                            \
                   return launch_onepass_scan<int16_t, int32_t, 1, 8, U, 0>(x, y, nullptr, n, k, s, g_ws);      \
