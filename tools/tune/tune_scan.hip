@@ -321,6 +321,12 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   AH(4, 1, 512, 2, 1)
   AH(8, 1, 512, 2, 1)
   AH(2, 1, 1024, 2, 1)
+#define AHR(U, W)                                                                                       \
+  vs.push_back({"ahead rc U" #U " w" #W, true, [=](hipStream_t s) {                                       \
+                  return launch_ahead_scan<float, double, 1, 4, U, 1, 2, true, W>(x, y, nullptr, n, k, s, g_ws, 512); \
+                }});
+  AHR(4, 1)
+  AHR(8, 1)
 #define OP(U, NT)                                                                                       \
   vs.push_back({"onepass U" #U " NT" #NT, true, [=](hipStream_t s) {                                      \
                   return launch_onepass_scan<float, double, 1, 4, U, NT>(x, y, nullptr, n, k, s, g_ws);        \
@@ -446,7 +452,14 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                 }});
     SAH(4, 512, 1, 2)
     SAH(2, 1024, 1, 2)
-    SAH(8, 512, 1, 2)
+#define SAHR(U, W)                                                                                      \
+  vs.push_back({"i16 stereo ahead rc U" #U " w" #W, true, [=](hipStream_t s) {                            \
+                  return launch_ahead_scan<int16_t, int32_t, 2, 4, U, 1, 2, true, W>(x, y, nullptr, n / 2, k, s, g_ws, 512); \
+                }});
+    SAHR(4, 1)
+    SAHR(4, 6)
+    SAHR(2, 1)
+    SAHR(8, 1)
 #define SOP(U)                                                                                          \
   vs.push_back({"i16 stereo onepass U" #U, true, [=](hipStream_t s) {                                     \
                   return launch_onepass_scan<int16_t, int32_t, 2, 4, U, 0>(x, y, nullptr, n / 2, k, s, g_ws); \
@@ -533,7 +546,14 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                 }});
   IAH(4, 512, 1, 2)
   IAH(2, 1024, 1, 2)
-  IAH(8, 512, 1, 2)
+#define IAHR(U, W)                                                                                      \
+  vs.push_back({"i16 ahead rc U" #U " w" #W, true, [=](hipStream_t s) {                                   \
+                  return launch_ahead_scan<int16_t, int32_t, 1, 8, U, 1, 2, true, W>(x, y, nullptr, n, k, s, g_ws, 512); \
+                }});
+  IAHR(4, 1)
+  IAHR(4, 6)
+  IAHR(2, 1)
+  IAHR(8, 1)
 #define IOP(U)                                                                                          \
   vs.push_back({"i16 onepass U" #U, true, [=](hipStream_t s) {                                            \
                   return launch_onepass_scan<int16_t, int32_t, 1, 8, U, 0>(x, y, nullptr, n, k, s, g_ws);      \
