@@ -452,6 +452,16 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                 }});
     SAH(4, 512, 1, 2)
     SAH(2, 1024, 1, 2)
+#define SAH64(U, D)                                                                                     \
+  vs.push_back({"i16 stereo ahead i64 U" #U " D" #D, true, [=](hipStream_t s) {                           \
+                  return launch_ahead_scan<int16_t, int64_t, 2, 4, U, 1, 2, false, 1>(x, y, nullptr, n / 2, k, s, g_ws, D); \
+                }});
+    if (k > 65535) {
+      SAH64(4, 512)
+      SAH64(2, 1024)
+      SAH64(2, 512)
+      SAH64(1, 1024)
+    }
 #define SAHR(U, W)                                                                                      \
   vs.push_back({"i16 stereo ahead rc U" #U " w" #W, true, [=](hipStream_t s) {                            \
                   return launch_ahead_scan<int16_t, int32_t, 2, 4, U, 1, 2, true, W>(x, y, nullptr, n / 2, k, s, g_ws, 512); \
@@ -546,6 +556,16 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                 }});
   IAH(4, 512, 1, 2)
   IAH(2, 1024, 1, 2)
+#define IAH64(U, D)                                                                                     \
+  vs.push_back({"i16 ahead i64 U" #U " D" #D, true, [=](hipStream_t s) {                                  \
+                  return launch_ahead_scan<int16_t, int64_t, 1, 8, U, 1, 2, false, 1>(x, y, nullptr, n, k, s, g_ws, D); \
+                }});
+  if (k > 65535) {
+    IAH64(4, 512)
+    IAH64(2, 1024)
+    IAH64(2, 512)
+    IAH64(1, 1024)
+  }
 #define IAHR(U, W)                                                                                      \
   vs.push_back({"i16 ahead rc U" #U " w" #W, true, [=](hipStream_t s) {                                   \
                   return launch_ahead_scan<int16_t, int32_t, 1, 8, U, 1, 2, true, W>(x, y, nullptr, n, k, s, g_ws, 512); \
