@@ -52,9 +52,7 @@ __device__ __forceinline__ void stage_shifted_store(T* stage, const Unit<T, F * 
   for (int u = 0; u < U; ++u) IO::store(stage + (u * WG + tid) * VE, h[u]);
   if (tid == 0) IO::store(stage + (U * WG) * VE, h[U]);
 }
-// Stage the shifted tile [h0, h0 + (U*WG+1)*F) frames in LDS: every lane's
-// U units are loaded before any is stored (one memory round trip, not one per
-// unit), plus one extra unit for the misaligned x[n-k] read.
+// Both halves in one call (ORD 0/1).
 template <typename T, int C, int F, int U, int WG, int NT>
 __device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, const T* __restrict__ hist,
                                                    T* stage, long long h0, long long nframes, int k, int tid) {
@@ -73,8 +71,7 @@ __device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, con
 // peak (tools/tune/onepass_experiment.hpp): the tiles a window reaches back to
 // were dispatched only m*8 workgroups earlier (m = k/T), well inside the
 // ~2,000 workgroups in flight, so consumers wait on producers that are still
-// loading.  Here the workgroup of tile t publishes the sums of tile t + D
-// Here the workgroup in dispatch slot b publishes the sums of the tile of
+// loading.  Here the workgroup in dispatch slot b publishes the sums of the tile of
 // slot b + D ("look-ahead") before it scans its own tile:
 //   phase A  every wave loads its share of that tile (default policy, so the
 //            lines stay in the XCD's L2 / the MALL) and publishes its partial
