@@ -186,7 +186,8 @@ constexpr size_t ahead_granule_bytes(long long nfull) {
   // + 16 bytes of launch statistics (MAVG_AHEAD_STATS builds only)
   return (((size_t)(nfull > 0 ? nfull : 1) * kNW * C * GranCount<SA>::n * 8) + 15) / 16 * 16 + 16;
 }
-template <typename T, typename A, int C, int F, int U, int NT = kNtStore, int ORD = 2, bool RC = false, int WPS = 1>
+template <typename T, typename A, int C, int F, int U, int NT = kNtStore, int ORD = 2, bool RC = false, int WPS = 1,
+          int PF = 0>
 int launch_ahead_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
                       Workspace ws, int ahead = -1, int spin = -1) {
   if (ahead < 0) ahead = ahead_knob("MAVG_AHEAD_SLOTS", kAheadSlots, 0, 1 << 30) & ~7;
@@ -201,13 +202,17 @@ int launch_ahead_scan(const void* in, void* out, const void* hist, long long nfr
   const long long nfull = nframes / TF;
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   const size_t need = ahead_granule_bytes<T, A, C, F, U>(nfull);
+  // PF = 0: 4 prefetched record rounds when a window spans more than one
+  // round of kWG records (k / T + 1 whole tiles x kNW records), else 1
+  const long long max_records = ((long long)k / TF + 1) * kNW;
+  const int pf = PF != 0 ? PF : (max_records > kWG ? 4 : 1);
   const size_t lds = kStageBytes + (size_t)kNW * C * sizeof(A) + (size_t)NSEG * C * sizeof(SA);
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
+             "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d,pf=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
              "ahead=%d remap=%d ws=%zu",
-             type_name<T>(), type_name<A>(), C, F, U, NT, ntiles, kWG, lds, TF, ahead, xcd_remap, need);
+             type_name<T>(), type_name<A>(), C, F, U, NT, pf, ntiles, kWG, lds, TF, ahead, xcd_remap, need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -230,7 +235,12 @@ int launch_ahead_scan(const void* in, void* out, const void* hist, long long nfr
   p.spin = spin;
   p.gran = static_cast<unsigned long long*>(ws.ptr);
   p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
-  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, ORD, RC, WPS>), dim3((unsigned)ntiles), dim3(kWG), lds, st, p);
+  if (pf == 4)
+    hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, ORD, RC, WPS, 4>), dim3((unsigned)ntiles), dim3(kWG), lds,
+                       st, p);
+  else
+    hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, ORD, RC, WPS, 1>), dim3((unsigned)ntiles), dim3(kWG), lds,
+                       st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 

@@ -179,7 +179,10 @@ struct AheadParams {
 // ORD: 0 = phase A, then the tile and the stage; 1 = phase A loads, tile
 // loads, phase A record, stage; 2 = tile, stage and phase A loads all in
 // flight, then the stage stores and the phase A record
-template <typename T, typename A, int C, int F, int U, int NT, int ORD = 2, bool RC = false, int WPS = 1>
+// PF: rounds of WG records whose loads are all issued before the barrier
+// (1, or 4 for windows spanning more than WG records: the rounds are then not
+// a chain of dependent L2 round trips)
+template <typename T, typename A, int C, int F, int U, int NT, int ORD = 2, bool RC = false, int WPS = 1, int PF = 1>
 __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   constexpr int WG = kWG;
   constexpr int NW = WG / 64;
@@ -292,14 +295,15 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
       }
     }
   }
-  // first round of record loads (checked after the in-tile scan)
-  unsigned long long rv[C][NG];
-  {
-    const long long q = qlo + tid;
+  // first PF rounds of record loads (checked after the in-tile scan)
+  unsigned long long rvp[PF][C][NG];
+#pragma unroll
+  for (int r = 0; r < PF; ++r) {
+    const long long q = qlo + (long long)r * WG + tid;
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int h = 0; h < NG; ++h) rv[c][h] = q < qhi ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
+      for (int h = 0; h < NG; ++h) rvp[r][c][h] = q < qhi ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
   }
   __syncthreads();
 
@@ -379,10 +383,20 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   A hq[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) hq[c] = (A)0;
-  for (long long qb = qlo; qb < qhi; qb += WG) {
+  int ri = 0;
+  for (long long qb = qlo; qb < qhi; qb += WG, ++ri) {
     const long long q = qb + tid;
     const bool act = q < qhi;
-    if (qb != qlo) {
+    unsigned long long rv[C][NG];
+    if (ri < PF) {
+#pragma unroll
+      for (int r = 0; r < PF; ++r)  // static register selection, no indexed scratch
+        if (r == ri)
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int h = 0; h < NG; ++h) rv[c][h] = rvp[r][c][h];
+    } else {
 #pragma unroll
       for (int c = 0; c < C; ++c)
 #pragma unroll

@@ -53,8 +53,8 @@ def plan_key(plan):
         args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["nt"], wg, "true" if kv.get("rc", "1") == "1" else "false")
     elif fam == "direct":
         args = (T, acc, kv["C"], kv["F"], kv["U"], wg)
-    elif fam == "ahead_scan":  # ORD=2, RC=false, WPS=1: the only instantiation the dispatch makes
-        args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], "2", "false", "1")
+    elif fam == "ahead_scan":  # ORD=2, RC=false, WPS=1 (the dispatch's only choice); PF from the plan
+        args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], "2", "false", "1", kv.get("pf", "1"))
     elif fam == "segment_scan":
         args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["pd"], kv["nt"])
     else:

@@ -319,6 +319,12 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
                   return launch_ahead_scan<float, double, 1, 4, U, NT, ORD, false, WPS>(x, y, nullptr, n, k, s, g_ws, D); \
                 }});
   AH(4, 1, 512, 2, 1)
+#define AHP(PF)                                                                                         \
+  vs.push_back({"ahead U4 pf" #PF, true, [=](hipStream_t s) {                                             \
+                  return launch_ahead_scan<float, double, 1, 4, 4, 1, 2, false, 1, PF>(x, y, nullptr, n, k, s, g_ws, 512); \
+                }});
+  AHP(1)
+  AHP(4)
   AH(8, 1, 512, 2, 1)
   AH(2, 1, 1024, 2, 1)
 #define AHR(U, W)                                                                                       \
@@ -562,6 +568,12 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                 }});
   if (k > 65535) {
     IAH64(4, 512)
+    vs.push_back({"i16 ahead i64 U4 pf1", true, [=](hipStream_t s) {
+                    return launch_ahead_scan<int16_t, int64_t, 1, 8, 4, 1, 2, false, 1, 1>(x, y, nullptr, n, k, s, g_ws, 512);
+                  }});
+    vs.push_back({"i16 ahead i64 U4 pf4", true, [=](hipStream_t s) {
+                    return launch_ahead_scan<int16_t, int64_t, 1, 8, 4, 1, 2, false, 1, 4>(x, y, nullptr, n, k, s, g_ws, 512);
+                  }});
     IAH64(2, 1024)
     IAH64(2, 512)
     IAH64(1, 1024)
