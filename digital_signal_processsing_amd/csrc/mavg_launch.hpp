@@ -184,7 +184,7 @@ template <typename T, typename A, int C, int F, int U>
 constexpr size_t ahead_granule_bytes(long long nfull) {
   using SA = typename ScanAcc<T, A>::type;
   // + 16 bytes of launch statistics (MAVG_AHEAD_STATS builds only)
-  return (((size_t)(nfull > 0 ? nfull : 1) * kNW * C * GranCount<SA>::n * 8) + 15) / 16 * 16 + 16;
+  return (((size_t)(nfull > 0 ? nfull : 1) * C * GranCount<SA>::n * 8) + 15) / 16 * 16 + 16;
 }
 template <typename T, typename A, int C, int F, int U, int NT = kNtStore, int ORD = 2, bool RC = false, int WPS = 1,
           int PF = 0>
@@ -203,10 +203,12 @@ int launch_ahead_scan(const void* in, void* out, const void* hist, long long nfr
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   const size_t need = ahead_granule_bytes<T, A, C, F, U>(nfull);
   // PF = 0: 4 prefetched record rounds when a window spans more than one
-  // round of kWG records (k / T + 1 whole tiles x kNW records), else 1
-  const long long max_records = ((long long)k / TF + 1) * kNW;
-  const int pf = PF != 0 ? PF : (max_records > kWG ? 4 : 1);
-  const size_t lds = kStageBytes + (size_t)kNW * C * sizeof(A) + (size_t)NSEG * C * sizeof(SA);
+  // round of kWG records (one per whole tile: k / T + 1) or C == 1, else 1
+  const long long max_records = (long long)k / TF + 1;
+  // mono also below one round: 4 measured faster (fp32 k=8192 0.72 vs 0.69,
+  // int16 k=30000 0.56 vs 0.53); stereo 1 (0.59 vs 0.575, sweep_records.sh)
+  const int pf = PF != 0 ? PF : (max_records > kWG || C == 1 ? 4 : 1);
+  const size_t lds = kStageBytes + (size_t)kNW * C * sizeof(A) + (size_t)(NSEG + 3 * kNW) * C * sizeof(SA);
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),

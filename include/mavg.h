@@ -79,8 +79,8 @@ typedef enum {
 /* Device workspace (bytes) mavg_run needs for this problem.  0 for every
  * launch except the look-ahead scan that AUTO/BLELLOCH pick for windows too
  * long for an LDS-staged halo (fp32 halos > 16 KiB, e.g. mono k > 4096;
- * int16 past ~47 KiB): 8 B per (whole tile, wave, channel, 32-bit word of
- * the tile sum), padded to 16, + 16 (16 MiB for 2^30 fp32 samples).
+ * int16 past ~47 KiB): 8 B per (whole tile, channel, 32-bit word of the
+ * tile sum), padded to 16, + 16 (4 MiB for 2^30 fp32 samples).
  * 16-B alignment; contents need no initialisation (mavg_run zeroes them on
  * the stream); one workspace must not serve two launches that may run
  * concurrently. */

@@ -115,21 +115,21 @@ def test_plan_describes_launch_without_gpu():
 def test_workspace_only_for_ahead_scan():
     import digital_signal_processsing_amd as dsp
     # halo-staged tiles need none; the look-ahead scan needs its record
-    # granules: 8 bytes per (whole tile, wave, channel, 32-bit word of the
-    # tile-sum type), padded to 16 bytes, plus 16 bytes of statistics
+    # granules: 8 bytes per (whole tile, channel, 32-bit word of the tile-sum
+    # type), padded to 16 bytes, plus 16 bytes of statistics
     assert dsp.workspace_bytes(1 << 30, 1024) == 0
     assert dsp.workspace_bytes(1 << 30, 4096) == 0
     # fp32 halos past 16 KiB take the look-ahead scan (U=4: 4096-frame tiles)
     tiles = (1 << 30) // 4096
     assert dsp.plan(1 << 30, 8192).startswith("ahead_scan<f32,acc=f64,C=1,F=4,U=4")
-    assert dsp.workspace_bytes(1 << 30, 8192) == tiles * 4 * 2 * 8 + 16
-    assert "ws=%d" % (tiles * 4 * 2 * 8 + 16) in dsp.plan(1 << 30, 20_000)
+    assert dsp.workspace_bytes(1 << 30, 8192) == tiles * 2 * 8 + 16
+    assert "ws=%d" % (tiles * 2 * 8 + 16) in dsp.plan(1 << 30, 20_000)
     assert dsp.plan(1 << 30, 8192, algo="hillis").startswith("segment_scan<")
     # int16 keeps the 1024-thread tile up to ~47 KiB of halo
     assert dsp.workspace_bytes(1 << 30, 8192, dtype=dsp.I16) == 0
     n = 2 * 1_000_003
-    st = (n // 2) // 4096     # int16 stereo: one int32 word per (whole tile, wave, channel)
-    assert dsp.workspace_bytes(n, 44100, 2, dsp.I16) == (st * 4 * 2 * 8 + 15) // 16 * 16 + 16
+    st = (n // 2) // 4096     # int16 stereo: one int32 word per (whole tile, channel)
+    assert dsp.workspace_bytes(n, 44100, 2, dsp.I16) == (st * 2 * 8 + 15) // 16 * 16 + 16
     assert dsp.workspace_bytes(1 << 20, 70_000, algo="hillis") == 0
     assert dsp.workspace_bytes(0, 70_000) == 0
 

@@ -1,23 +1,26 @@
-// mavg_lookback.hpp -- the look-ahead scan (ahead_scan_kernel): windows too long for an
-// LDS-staged halo, carry from earlier tiles' sums published inside the launch.
+// ahead_wave_records.hpp -- tuner-only A/B copy of the look-ahead scan with
+// one record per (tile, WAVE) published before the barrier (the form before
+// per-tile records).  Not part of libmavg.
 #pragma once
 
-#include "mavg_device.hpp"
+#include "../../digital_signal_processsing_amd/csrc/mavg_launch.hpp"
 
-namespace mavg {
+namespace mavg_wave {
+using namespace mavg;
+
 
 // Accumulator of the in-tile scan: the prefix of d = x - x[n-k] over one
 // tile telescopes to two sums of at most T samples, |.| <= 2 * T * 32768 <=
 // 2^28 for int16 tiles, so it fits int32 even when the window sum (the
 // carry) needs int64 (k > 65535).
-template <typename T, typename A> struct ScanAcc { using type = A; };
-template <> struct ScanAcc<int16_t, int64_t> { using type = int32_t; };
+template <typename T, typename A> struct ScanAcc_w { using type = A; };
+template <> struct ScanAcc_w<int16_t, int64_t> { using type = int32_t; };
 
 // Stage the shifted tile [h0, h0 + (U*WG+1)*F) frames in LDS: every lane's
 // U units are loaded before any is stored (one memory round trip, not one per
 // unit), plus one extra unit for the misaligned x[n-k] read.
 template <typename T, int C, int F, int U, int WG, int NT>
-__device__ __forceinline__ void stage_shifted_load(const T* __restrict__ in, const T* __restrict__ hist,
+__device__ __forceinline__ void stage_shifted_load_w(const T* __restrict__ in, const T* __restrict__ hist,
                                                    Unit<T, F * C> (&h)[U + 1], long long h0, long long nframes,
                                                    int k, int tid) {
   constexpr int VE = F * C;
@@ -45,7 +48,7 @@ __device__ __forceinline__ void stage_shifted_load(const T* __restrict__ in, con
   }
 }
 template <typename T, int C, int F, int U, int WG>
-__device__ __forceinline__ void stage_shifted_store(T* stage, const Unit<T, F * C> (&h)[U + 1], int tid) {
+__device__ __forceinline__ void stage_shifted_store_w(T* stage, const Unit<T, F * C> (&h)[U + 1], int tid) {
   constexpr int VE = F * C;
   using IO = UnitIO<T, VE>;
 #pragma unroll
@@ -54,11 +57,11 @@ __device__ __forceinline__ void stage_shifted_store(T* stage, const Unit<T, F * 
 }
 // Both halves in one call (ORD 0/1).
 template <typename T, int C, int F, int U, int WG, int NT>
-__device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, const T* __restrict__ hist,
+__device__ __forceinline__ void stage_shifted_tile_w(const T* __restrict__ in, const T* __restrict__ hist,
                                                    T* stage, long long h0, long long nframes, int k, int tid) {
   Unit<T, F * C> h[U + 1];
-  stage_shifted_load<T, C, F, U, WG, NT>(in, hist, h, h0, nframes, k, tid);
-  stage_shifted_store<T, C, F, U, WG>(stage, h, tid);
+  stage_shifted_load_w<T, C, F, U, WG, NT>(in, hist, h, h0, nframes, k, tid);
+  stage_shifted_store_w<T, C, F, U, WG>(stage, h, tid);
 }
 
 // ----------------------------------------------------------------------------
@@ -74,12 +77,10 @@ __device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, con
 // loading.  Here the workgroup in dispatch slot b publishes the sums of the tile of
 // slot b + D ("look-ahead") before it scans its own tile:
 //   phase A  every wave loads its share of that tile (default policy, so the
-//            lines stay in the XCD's L2 / the MALL) and leaves its partial sum
-//            in LDS; after the block's first barrier one wave adds the NW
-//            partials in wave order and publishes the tile's record as 8-byte
-//            {tag, 32-bit payload} granules with agent-scope (sc1) stores
-//            (cdna_hip_programming.md Guideline 16, R2: the data is the flag,
-//            no fences); slots b < D publish their own tiles';
+//            lines stay in the XCD's L2 / the MALL) and publishes its partial
+//            sum as 8-byte {tag, 32-bit payload} granules with agent-scope
+//            (sc1) stores (cdna_hip_programming.md Guideline 16, R2: the data
+//            is the flag, no fences); slots b < D publish their own tiles';
 //   phase B  the tile-scan of lookback_scan_kernel, its whole-tile carry read
 //            from the granules with sc1 loads.  The tiles run in remap mode 1
 //            (one contiguous run per XCD), so slot b + D is on b's XCD and
@@ -99,35 +100,34 @@ __device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, con
 // tag is never stale, also under graph replay (Guideline 16, "Re-initialise
 // every call").  The carry adds the records in a fixed order: deterministic.
 // ----------------------------------------------------------------------------
-typedef __attribute__((address_space(1))) unsigned long long gran_t;  // global, never flat
-constexpr unsigned long long kGranTag = 1ull << 32;                   // tag 1 in the high word (0 = empty)
+typedef __attribute__((address_space(1))) unsigned long long gran_t_w;  // global, never flat
+constexpr unsigned long long kGranTag_w = 1ull << 32;                   // tag 1 in the high word (0 = empty)
 
 // granules per record value: a 32-bit payload each
-template <typename SA> struct GranCount { static constexpr int n = sizeof(SA) / 4; };
+template <typename SA> struct GranCount_w { static constexpr int n = sizeof(SA) / 4; };
 
-__device__ __forceinline__ void gran_store(gran_t* g, uint32_t v) {
-  __hip_atomic_store(g, kGranTag | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // one sc1 8-B store
+__device__ __forceinline__ void gran_store_w(gran_t_w* g, uint32_t v) {
+  __hip_atomic_store(g, kGranTag_w | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // one sc1 8-B store
 }
-__device__ __forceinline__ unsigned long long gran_load(const gran_t* g) {
-  return __hip_atomic_load(const_cast<gran_t*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+__device__ __forceinline__ unsigned long long gran_load_w(const gran_t_w* g) {
+  return __hip_atomic_load(const_cast<gran_t_w*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
 }
-__device__ __forceinline__ uint32_t gran_word(double v, int h) {
+__device__ __forceinline__ uint32_t gran_word_w(double v, int h) {
   return h == 0 ? (uint32_t)__double2loint(v) : (uint32_t)__double2hiint(v);
 }
-__device__ __forceinline__ uint32_t gran_word(int32_t v, int) { return (uint32_t)v; }
-template <typename SA> __device__ __forceinline__ SA gran_value(const uint32_t (&w)[GranCount<SA>::n]);
-template <> __device__ __forceinline__ double gran_value<double>(const uint32_t (&w)[2]) {
+__device__ __forceinline__ uint32_t gran_word_w(int32_t v, int) { return (uint32_t)v; }
+template <typename SA> __device__ __forceinline__ SA gran_value_w(const uint32_t (&w)[GranCount_w<SA>::n]);
+template <> __device__ __forceinline__ double gran_value_w<double>(const uint32_t (&w)[2]) {
   return __hiloint2double((int)w[1], (int)w[0]);
 }
-template <> __device__ __forceinline__ int32_t gran_value<int32_t>(const uint32_t (&w)[1]) { return (int32_t)w[0]; }
+template <> __device__ __forceinline__ int32_t gran_value_w<int32_t>(const uint32_t (&w)[1]) { return (int32_t)w[0]; }
 
-// One wave's share of a tile's sum (wave slot wv): lane l sums its units
-// u*WG + wv*64 + l over u, frames and channels in order, then one DPP wave
-// scan.  A tile's record is its NW shares added in wave order.  Producers
-// (phase A), tiles t < D (own registers), head duty and the recompute path
-// all run this sequence: bitwise the same value.
+// One wave's share of a tile's sum ("record" of wave slot wv): lane l sums its
+// units u*WG + wv*64 + l over u, frames and channels in order, then one DPP
+// wave scan.  Producers (phase A), tiles t < D (own registers) and the
+// recompute path all run this sequence: bitwise the same value.
 template <typename T, typename SA, int C, int F, int U>
-__device__ __forceinline__ void wave_record(const Unit<T, F * C> (&x)[U], SA (&r)[C]) {
+__device__ __forceinline__ void wave_record_w(const Unit<T, F * C> (&x)[U], SA (&r)[C]) {
   SA ls[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) ls[c] = (SA)0;
@@ -141,27 +141,27 @@ __device__ __forceinline__ void wave_record(const Unit<T, F * C> (&x)[U], SA (&r
   for (int c = 0; c < C; ++c) r[c] = readlane(wave_incl_scan(ls[c]), 63);
 }
 
-// lanes 0 .. C*NG-1 of the wave each store one granule of tile j's record
-template <typename SA, int C>
-__device__ __forceinline__ void publish_record(gran_t* gran, long long j, const SA (&r)[C], int lane) {
-  constexpr int NG = GranCount<SA>::n;
+// lanes 0 .. C*NG-1 of the wave each store one granule of record (j, wv)
+template <typename SA, int C, int NW>
+__device__ __forceinline__ void publish_record_w(gran_t_w* gran, long long j, int wv, const SA (&r)[C], int lane) {
+  constexpr int NG = GranCount_w<SA>::n;
   if (lane < C * NG) {
     const int c = lane / NG, h = lane - c * NG;
     SA v = r[0];
 #pragma unroll
     for (int i = 1; i < C; ++i)
       if (c == i) v = r[i];
-    gran_store(gran + (j * C + c) * NG + h, gran_word(v, h));
+    gran_store_w(gran + ((j * NW + wv) * C + c) * NG + h, gran_word_w(v, h));
   }
 }
 
 // first tile of XCD run x under remap mode 1 (remap_tile)
-__device__ __forceinline__ long long run_start(unsigned x, unsigned nb) {
+__device__ __forceinline__ long long run_start_w(unsigned x, unsigned nb) {
   const unsigned q = nb >> 3, r = nb & 7u;
   return (long long)(x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q);
 }
 
-struct AheadParams {
+struct AheadParams_w {
   const void* in;
   void* out;
   const void* hist;
@@ -174,7 +174,7 @@ struct AheadParams {
   int ahead;        // D (a multiple of 8): block b publishes the records of block b + D's tile
   int head;         // whole tiles a window can span (k / T): the head duty of remap mode 1
   int spin;         // polls of an untagged granule before recomputing it
-  unsigned long long* gran;  // [nfull][C][NG] granules, zeroed before the launch
+  unsigned long long* gran;  // [nfull][NW][C][NG] granules, zeroed before the launch
   void* stats;               // MAVG_AHEAD_STATS builds only: {recomputes, polls that waited}
   OutParams o;
 };
@@ -186,7 +186,7 @@ struct AheadParams {
 // (1, or 4 for windows spanning more than WG records: the rounds are then not
 // a chain of dependent L2 round trips)
 template <typename T, typename A, int C, int F, int U, int NT, int ORD = 2, bool RC = false, int WPS = 1, int PF = 1>
-__global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
+__global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel_w(AheadParams_w p) {
   constexpr int WG = kWG;
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
@@ -196,19 +196,18 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   constexpr int kStageBytes = ((kStageUnits * VE * (int)sizeof(T)) + 15) & ~15;
   using IO = UnitIO<T, VE>;
   using U_t = Unit<T, VE>;
-  using SA = typename ScanAcc<T, A>::type;
-  constexpr int NG = GranCount<SA>::n;
+  using SA = typename ScanAcc_w<T, A>::type;
+  constexpr int NG = GranCount_w<SA>::n;
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* stage = reinterpret_cast<T*>(smem);
   A* hsum = reinterpret_cast<A*>(smem + kStageBytes);  // [NW][C] carry partials
   SA* tot = reinterpret_cast<SA*>(hsum + NW * C);       // [NSEG][C] segment totals
-  SA* shares = tot + NSEG * C;                           // [3][NW][C] wave shares of the records published here
 
   const T* __restrict__ in = static_cast<const T*>(p.in);
   T* __restrict__ out = static_cast<T*>(p.out);
   const T* __restrict__ hist = static_cast<const T*>(p.hist);
-  gran_t* gran = (gran_t*)p.gran;
+  gran_t_w* gran = (gran_t_w*)p.gran;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = tid >> 6;
@@ -222,7 +221,7 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   const bool tile_full = (t0 + TF <= nframes);
   const long long a = t0 - k;
   const long long jlo = a >= 0 ? (a + TF - 1) / TF : 0;
-  const long long qlo = jlo, qhi = tile;  // records of the whole tiles [jlo, tile)
+  const long long qlo = jlo * NW, qhi = tile * NW;  // records of the whole tiles [jlo, tile)
 
   // ---- phase A (this wave's share of tile t + D -> record) and phase B's
   //      loads: the tile (an L2 / MALL hit: phase A of tile t-D) and the
@@ -237,18 +236,11 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
 #pragma unroll
       for (int u = 0; u < U; ++u) xa[u] = IO::load(in + (ja * TF + (long long)(u * WG + tid) * F) * C);
   };
-  // source 0 = phase A (tile ja), 1 = own tile, 2 = head duty: each wave
-  // leaves its share in LDS, published after the first barrier
-  auto share = [&](int src, const SA (&r)[C]) {
-    if (lane == 0)
-#pragma unroll
-      for (int c = 0; c < C; ++c) shares[(src * NW + w) * C + c] = r[c];
-  };
   auto publish_a = [&]() {
     if (produce) {
       SA r[C];
-      wave_record<T, SA, C, F, U>(xa, r);
-      share(0, r);
+      wave_record_w<T, SA, C, F, U>(xa, r);
+      publish_record_w<SA, C, NW>(gran, ja, w, r, lane);
     }
   };
   U_t x[U];
@@ -270,44 +262,41 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
     load_a();
     publish_a();
     load_tile();
-    stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, tid);
+    stage_shifted_tile_w<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, tid);
   } else if constexpr (ORD == 1) {
     load_a();
     load_tile();
     publish_a();
-    stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, tid);
+    stage_shifted_tile_w<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, tid);
   } else {
     U_t hs[U + 1];
     load_tile();
-    stage_shifted_load<T, C, F, U, WG, NT>(in, hist, hs, h0, nframes, k, tid);
+    stage_shifted_load_w<T, C, F, U, WG, NT>(in, hist, hs, h0, nframes, k, tid);
     load_a();
-    stage_shifted_store<T, C, F, U, WG>(stage, hs, tid);
+    stage_shifted_store_w<T, C, F, U, WG>(stage, hs, tid);
     publish_a();
   }
-  const bool own = blockIdx.x < (unsigned)p.ahead && tile < p.nfull;  // no block D slots earlier
-  if (own) {
+  if (blockIdx.x < (unsigned)p.ahead && tile < p.nfull) {  // no block D slots earlier: the tile itself
     SA r[C];
-    wave_record<T, SA, C, F, U>(x, r);
-    share(1, r);
+    wave_record_w<T, SA, C, F, U>(x, r);
+    publish_record_w<SA, C, NW>(gran, tile, w, r, lane);
   }
   // head duty (remap mode 1): the first tiles of XCD run x need the records of
   // the last tiles of run x-1, whose blocks are dispatched at the end of the
   // grid; the first `head` blocks of run x publish those records instead
-  long long jh = -1;
   if (p.xcd_remap == 1) {
     const unsigned xr = blockIdx.x & 7u, s = blockIdx.x >> 3;
     if (xr >= 1u && s < (unsigned)p.head) {
-      const long long j = run_start(xr, nb) - p.head + s;
-      if (j >= 0 && j < p.nfull) jh = j;
-    }
-  }
-  if (jh >= 0) {
-    U_t xh[U];
+      const long long j = run_start_w(xr, nb) - p.head + s;
+      if (j >= 0 && j < p.nfull) {
+        U_t xh[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) xh[u] = IO::load(in + (jh * TF + (long long)(u * WG + tid) * F) * C);
-    SA r[C];
-    wave_record<T, SA, C, F, U>(xh, r);
-    share(2, r);
+        for (int u = 0; u < U; ++u) xh[u] = IO::load(in + (j * TF + (long long)(u * WG + tid) * F) * C);
+        SA r[C];
+        wave_record_w<T, SA, C, F, U>(xh, r);
+        publish_record_w<SA, C, NW>(gran, j, w, r, lane);
+      }
+    }
   }
   // first PF rounds of record loads (checked after the in-tile scan)
   unsigned long long rvp[PF][C][NG];
@@ -317,24 +306,9 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int h = 0; h < NG; ++h) rvp[r][c][h] = q < qhi ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
+      for (int h = 0; h < NG; ++h) rvp[r][c][h] = q < qhi ? gran_load_w(gran + (q * C + c) * NG + h) : 0ull;
   }
   __syncthreads();
-  // publish the records whose wave shares this block holds: wave src adds
-  // source src's NW shares in wave order
-  if (w < 3) {
-    const long long j = w == 0 ? (produce ? ja : -1) : (w == 1 ? (own ? tile : -1) : jh);
-    if (j >= 0) {
-      SA r[C];
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        r[c] = shares[(w * NW) * C + c];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) r[c] += shares[(w * NW + i) * C + c];
-      }
-      publish_record<SA, C>(gran, j, r, lane);
-    }
-  }
 
   // ---- partial carry: the part of [a, t0) before the first whole tile ----
   A hp[C];
@@ -429,7 +403,7 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
 #pragma unroll
       for (int c = 0; c < C; ++c)
 #pragma unroll
-        for (int h = 0; h < NG; ++h) rv[c][h] = act ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
+        for (int h = 0; h < NG; ++h) rv[c][h] = act ? gran_load_w(gran + (q * C + c) * NG + h) : 0ull;
     }
     for (int it = 0;; ++it) {
       bool miss = false;
@@ -446,7 +420,7 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
 #pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
-          for (int h = 0; h < NG; ++h) rv[c][h] = gran_load(gran + (q * C + c) * NG + h);
+          for (int h = 0; h < NG; ++h) rv[c][h] = gran_load_w(gran + (q * C + c) * NG + h);
     }
     bool miss = false;
 #pragma unroll
@@ -458,22 +432,19 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
     while (mask != 0ull) {
       const int l = __builtin_ctzll(mask);
       mask &= mask - 1ull;
-      const long long jj = __shfl(q, l, 64);  // the tile whose record is missing
+      const long long qq = __shfl(q, l, 64);
+      const long long jj = qq / NW;
+      const int wv = (int)(qq - jj * NW);
+      U_t xr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) xr[u] = IO::load(in + (jj * TF + (long long)(u * WG + wv * 64 + lane) * F) * C);
       SA r[C];
-      for (int wv = 0; wv < NW; ++wv) {  // its NW wave shares, in wave order
-        U_t xr[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) xr[u] = IO::load(in + (jj * TF + (long long)(u * WG + wv * 64 + lane) * F) * C);
-        SA rw[C];
-        wave_record<T, SA, C, F, U>(xr, rw);
-#pragma unroll
-        for (int c = 0; c < C; ++c) r[c] = wv == 0 ? rw[c] : r[c] + rw[c];
-      }
+      wave_record_w<T, SA, C, F, U>(xr, r);
       if (lane == l)
 #pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
-          for (int h = 0; h < NG; ++h) rv[c][h] = kGranTag | gran_word(r[c], h);
+          for (int h = 0; h < NG; ++h) rv[c][h] = kGranTag_w | gran_word_w(r[c], h);
 #ifdef MAVG_AHEAD_STATS
       if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats), 1u);
 #endif
@@ -484,7 +455,7 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
         uint32_t wd[NG];
 #pragma unroll
         for (int h = 0; h < NG; ++h) wd[h] = (uint32_t)rv[c][h];
-        hq[c] += (A)gran_value<SA>(wd);
+        hq[c] += (A)gran_value_w<SA>(wd);
       }
   }
 #pragma unroll
@@ -543,4 +514,69 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   }
 }
 
-}  // namespace mavg
+
+template <typename T, typename A, int C, int F, int U>
+constexpr size_t ahead_granule_bytes_w(long long nfull) {
+  using SA = typename ScanAcc_w<T, A>::type;
+  // + 16 bytes of launch statistics (MAVG_AHEAD_STATS builds only)
+  return (((size_t)(nfull > 0 ? nfull : 1) * kNW * C * GranCount_w<SA>::n * 8) + 15) / 16 * 16 + 16;
+}
+template <typename T, typename A, int C, int F, int U, int NT = kNtStore, int ORD = 2, bool RC = false, int WPS = 1,
+          int PF = 0>
+int launch_ahead_wave(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
+                      Workspace ws, int ahead = -1, int spin = -1) {
+  if (ahead < 0) ahead = ahead_knob("MAVG_AHEAD_SLOTS", kAheadSlots, 0, 1 << 30) & ~7;
+  if (spin < 0) spin = ahead_knob("MAVG_AHEAD_SPIN", kAheadSpin, 0, 1 << 20);
+  constexpr int xcd_remap = 1;  // one run per XCD (see ahead_scan_kernel_w)
+  constexpr int TF = kWG * F * U;
+  constexpr int VE = F * C;
+  constexpr int NSEG = U * kNW;
+  using SA = typename ScanAcc_w<T, A>::type;
+  constexpr size_t kStageBytes = (((size_t)(U * kWG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15;
+  const long long ntiles = (nframes + TF - 1) / TF;
+  const long long nfull = nframes / TF;
+  if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  const size_t need = ahead_granule_bytes_w<T, A, C, F, U>(nfull);
+  // PF = 0: 4 prefetched record rounds when a window spans more than one
+  // round of kWG records (k / T + 1 whole tiles x kNW records), else 1
+  const long long max_records = ((long long)k / TF + 1) * kNW;
+  const int pf = PF != 0 ? PF : (max_records > kWG ? 4 : 1);
+  const size_t lds = kStageBytes + (size_t)kNW * C * sizeof(A) + (size_t)NSEG * C * sizeof(SA);
+  if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text),
+             "ahead_wave<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d,pf=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
+             "ahead=%d remap=%d ws=%zu",
+             type_name<T>(), type_name<A>(), C, F, U, NT, pf, ntiles, kWG, lds, TF, ahead, xcd_remap, need);
+    g_plan->ws_bytes = need;
+    return MAVG_OK;
+  }
+  if (ws.ptr == nullptr || ws.bytes < need) return MAVG_ERR_WORKSPACE;
+  if ((reinterpret_cast<uintptr_t>(ws.ptr) & 15u) != 0) return MAVG_ERR_MISALIGNED;
+  if (hipMemsetAsync(ws.ptr, 0, need, st) != hipSuccess) return MAVG_ERR_HIP;
+  AheadParams_w p{};
+  p.in = in;
+  p.out = out;
+  p.hist = hist;
+  p.nframes = nframes;
+  p.nfull = nfull;
+  p.k = k;
+  p.o = make_out_params(k);
+  p.halo_units = (k + F - 1) / F;
+  p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
+  p.xcd_remap = xcd_remap;
+  p.ahead = ahead;
+  p.head = (int)std::min<long long>((long long)k / TF, nfull);
+  p.spin = spin;
+  p.gran = static_cast<unsigned long long*>(ws.ptr);
+  p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
+  if (pf == 4)
+    hipLaunchKernelGGL((ahead_scan_kernel_w<T, A, C, F, U, NT, ORD, RC, WPS, 4>), dim3((unsigned)ntiles), dim3(kWG), lds,
+                       st, p);
+  else
+    hipLaunchKernelGGL((ahead_scan_kernel_w<T, A, C, F, U, NT, ORD, RC, WPS, 1>), dim3((unsigned)ntiles), dim3(kWG), lds,
+                       st, p);
+  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+}
+
+}  // namespace mavg_wave
