@@ -326,6 +326,9 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
                 }});
   AHP(1)
   AHP(4)
+  vs.push_back({"ahead rc pf4", true, [=](hipStream_t s) {
+                  return launch_ahead_scan<float, double, 1, 4, 4, 1, 2, true, 1, 4>(x, y, nullptr, n, k, s, g_ws, 512);
+                }});
   vs.push_back({"ahead wave-records U4", true, [=](hipStream_t s) {
                   return mavg_wave::launch_ahead_wave<float, double, 1, 4, 4, 1, 2, false, 1, 0>(x, y, nullptr, n, k, s, g_ws, 512);
                 }});
@@ -461,6 +464,9 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                   return launch_ahead_scan<int16_t, int32_t, 2, 4, U, 1, ORD, false, W>(x, y, nullptr, n / 2, k, s, g_ws, D); \
                 }});
     SAH(4, 512, 1, 2)
+    vs.push_back({"i16 stereo ahead rc pf1", true, [=](hipStream_t s) {
+                    return launch_ahead_scan<int16_t, int32_t, 2, 4, 4, 1, 2, true, 1, 1>(x, y, nullptr, n / 2, k, s, g_ws, 512);
+                  }});
     vs.push_back({"i16 stereo ahead tile-records pf1", true, [=](hipStream_t s) {
                     return launch_ahead_scan<int16_t, int32_t, 2, 4, 4, 1, 2, false, 1, 1>(x, y, nullptr, n / 2, k, s, g_ws, 512);
                   }});
@@ -574,6 +580,9 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                   return launch_ahead_scan<int16_t, int32_t, 1, 8, U, 1, ORD, false, W>(x, y, nullptr, n, k, s, g_ws, D); \
                 }});
   IAH(4, 512, 1, 2)
+  vs.push_back({"i16 ahead rc pf4", true, [=](hipStream_t s) {
+                  return launch_ahead_scan<int16_t, int32_t, 1, 8, 4, 1, 2, true, 1, 4>(x, y, nullptr, n, k, s, g_ws, 512);
+                }});
   vs.push_back({"i16 ahead tile-records pf1", true, [=](hipStream_t s) {
                   return launch_ahead_scan<int16_t, int32_t, 1, 8, 4, 1, 2, false, 1, 1>(x, y, nullptr, n, k, s, g_ws, 512);
                 }});
