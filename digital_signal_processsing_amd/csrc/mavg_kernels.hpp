@@ -14,9 +14,10 @@
 //                      in LDS.  The default for windows up to ~16 KiB of halo.
 //   mavg_segment.hpp   scan_kernel: a workgroup walks a short segment chunk by
 //                      chunk with an LDS ring of the last k frames and a
-//                      k-frame pre-roll; longer windows, while the ring fits.
-//   mavg_lookback.hpp  tile_sums_kernel + lookback_scan_kernel: two passes,
-//                      carry from whole-tile sums; any k, same cost per sample.
+//                      k-frame pre-roll (the Hillis-Steele flavour's long windows).
+//   mavg_lookback.hpp  ahead_scan_kernel: one pass over HBM, carry from
+//                      whole-tile records that tiles 64 ahead published
+//                      inside the launch; windows past the LDS-staged halo.
 //   mavg_direct.hpp    direct_kernel: small windows summed directly from LDS
 //                      (replaces profilable_sm_*.cu).
 //   mavg_misc.hpp      naive_kernel (profilable_parallel_averager.cu:14-23)

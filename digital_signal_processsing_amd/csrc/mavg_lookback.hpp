@@ -80,7 +80,7 @@ __device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, con
 //            {tag, 32-bit payload} granules with agent-scope (sc1) stores
 //            (cdna_hip_programming.md Guideline 16, R2: the data is the flag,
 //            no fences); slots b < D publish their own tiles';
-//   phase B  the tile-scan of lookback_scan_kernel, its whole-tile carry read
+//   phase B  the tile scan (as tile_scan_kernel), its whole-tile carry read
 //            from the granules with sc1 loads.  The tiles run in remap mode 1
 //            (one contiguous run per XCD), so slot b + D is on b's XCD and
 //            holds b's tile + D/8: the consumers of a record run >= D slots
