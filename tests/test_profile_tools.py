@@ -1,0 +1,47 @@
+"""The profile tooling behind bench.py's `roofline.traffic` (tools/pmc_traffic.py):
+every bench workload's mavg_plan() string maps to the exact kernel template
+signature rocprofv3 reports, so each PMC dispatch is matched to its workload
+(several workloads share a grid size).  CPU only: the plans come from the
+library in plan mode, the kernel names are the ones in the committed traces."""
+import csv
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, ROOT)
+
+import pmc_traffic  # noqa: E402
+
+
+def test_kernel_key_parses_rocprof_names():
+    name = "void mavg::ahead_scan_kernel<float, double, 1, 4, 4, 1, 2, false, 1, 4>(mavg::AheadParams)"
+    assert pmc_traffic.kernel_key(name) == ("ahead_scan_kernel",
+                                            ("float", "double", "1", "4", "4", "1", "2", "false", "1", "4"))
+    assert pmc_traffic.kernel_key("__amd_rocclr_fillBufferAligned") is None
+
+
+def test_every_bench_workload_matches_a_traced_kernel():
+    """Each workload's plan maps to a kernel signature present in the
+    committed kernel trace summary (profiles/r01_kernel_trace_summary.csv)."""
+    import bench
+    import digital_signal_processsing_amd as dsp
+    traced = set()
+    with open(os.path.join(ROOT, "profiles", "r01_kernel_trace_summary.csv")) as f:
+        for row in csv.DictReader(f):
+            kk = pmc_traffic.kernel_key(row["kernel"])
+            if kk is not None:
+                traced.add(kk)
+    for name, (n, k, C, dt, algo) in bench.WORKLOADS.items():
+        plan = dsp.plan(n, k, C, dsp.F32 if dt == "f32" else dsp.I16, algo)
+        assert pmc_traffic.plan_key(plan) in traced, (name, plan)
+
+
+def test_traffic_json_covers_every_workload():
+    import json
+    import bench
+    t = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+    names = {key.split(":")[0] for key in t}
+    assert names == set(bench.WORKLOADS), sorted(set(bench.WORKLOADS) ^ names)
+    for v in t.values():
+        assert 0.99 < v["traffic_over_algorithmic"] < 1.05, v
