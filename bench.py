@@ -9,6 +9,7 @@ already resident in HBM (generated on the device by the counter-based
 synthetic generator).  Weak scaling: 2^30 samples per GPU.
 
     python bench.py                      # N=1, default K/W
+    python bench.py --gpus N             # spawns N ranks itself (one process per GPU)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Rank 0 prints ONE JSON line (contract in the task statement), with
@@ -20,7 +21,10 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -56,8 +60,9 @@ def parse():
     ap.add_argument("--workload", default="headline", choices=sorted(WORKLOADS))
     ap.add_argument("--algo", default=None, help="override the workload's algorithm")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-samples", type=int, default=1 << 28, help="bounded CPU-baseline sample (samples)")
-    ap.add_argument("--cpu-reps", type=int, default=10)
+    ap.add_argument("--cpu-samples", type=int, default=1 << 30,
+                    help="CPU-baseline sample (samples; default: the whole 2^30 headline signal, SURVEY.md 8d)")
+    ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0),
                     help="threads of the multi-core CPU baseline (default: OMP_NUM_THREADS, else os.cpu_count())")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -72,6 +77,55 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(base: dict, rank: int, world: int, port: int) -> dict:
+    """Environment of one self-launched rank (what torch.distributed.run sets)."""
+    env = dict(base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0",
+                "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    return env
+
+
+def self_launch(argv, world: int, timeout: float = None) -> int:
+    """`bench.py --gpus N` without a launcher: start N fresh child ranks (this
+    process has not touched the GPU and never does), wait for all of them and
+    return the worst exit status.  If one rank fails the others are stopped
+    (they would wait forever in the next collective).  Rank 0's stdout is the
+    one JSON line."""
+    port = _free_port()
+    me = os.path.abspath(__file__)
+    procs = [subprocess.Popen([sys.executable, "-u", me] + list(argv), env=rank_env(os.environ, r, world, port))
+             for r in range(world)]
+    deadline = None if timeout is None else time.monotonic() + timeout
+    worst = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            rc = 128 - rc if rc < 0 else rc
+            worst = max(worst, rc)
+            if rc != 0:
+                for q in live:  # the exact child PIDs this function started
+                    q.send_signal(signal.SIGTERM)
+        if deadline is not None and time.monotonic() > deadline:
+            for q in live:
+                q.kill()
+            worst = max(worst, 124)
+            deadline = None
+        time.sleep(0.05)
+    return worst
+
+
 def init_dist(args):
     import torch
     import torch.distributed as dist
@@ -79,8 +133,6 @@ def init_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.dist_backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
@@ -138,8 +190,10 @@ def cpu_model() -> str:
 
 def cpu_baseline(args, n_total, k, C, seed):
     """Oracle restatement (profilable_moving_averager.cpp:14-37, fp64 running
-    sum) on a bounded sample of the same synthetic stream, one host core
-    (the calling thread pinned to one allowed core)."""
+    sum) over the benchmark's own synthetic signal -- by default all of it
+    (2^30 samples at the headline, 3 reps) -- on one host core
+    (the calling thread pinned to one allowed core), then the OpenMP
+    restatement on `threads` cores pinned to the first allowed ones."""
     import oracle
     oracle.build()
     n = min(args.cpu_samples, n_total)
@@ -157,20 +211,28 @@ def cpu_baseline(args, n_total, k, C, seed):
     finally:
         os.sched_setaffinity(0, allowed)
     med = statistics.median(times)
-    threads = args.cpu_threads or os.cpu_count() or 1
-    oracle.mavg_f32_mt(x[: min(n, 1 << 20)], k, C, threads)
-    mt = []
-    for _ in range(max(3, args.cpu_reps // 2)):
-        t = time.perf_counter()
-        oracle.mavg_f32_mt(x, k, C, threads)
-        mt.append(time.perf_counter() - t)
+    threads = args.cpu_threads or len(allowed) or 1
+    pinned = sorted(allowed)[:threads]
+    # OpenMP creates its pool at the first parallel region (here), inheriting this mask
+    os.sched_setaffinity(0, set(pinned))
+    try:
+        oracle.mavg_f32_mt(x[: min(n, 1 << 20)], k, C, threads)
+        mt = []
+        for _ in range(max(3, args.cpu_reps)):
+            t = time.perf_counter()
+            oracle.mavg_f32_mt(x, k, C, threads)
+            mt.append(time.perf_counter() - t)
+    finally:
+        os.sched_setaffinity(0, allowed)
     mt_med = statistics.median(mt)
+    what = "the whole benchmark signal" if n == n_total else f"the first {n} of the benchmark's {n_total}"
     multicore = {
         "value": round(n / mt_med / 1e9, 4),
         "unit": "Gsamples/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"same sample, OpenMP chunks with a k-frame halo each, {threads} threads, "
+        "sample": f"same sample, OpenMP chunks with a k-frame halo each, {threads} threads pinned to cores "
+                  f"{_core_ranges(pinned)} (OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}), "
                   f"median of {len(mt)} reps, {mt_med * 1e3:.1f} ms/rep",
     }
     single = {
@@ -178,13 +240,29 @@ def cpu_baseline(args, n_total, k, C, seed):
         "unit": "Gsamples/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{n} fp32 samples (first {n} of the benchmark's synthetic stream), k={k}, C={C}, "
+        "sample": f"{n} fp32 samples ({what} synthetic samples), k={k}, C={C}, "
                   f"median of {args.cpu_reps} reps, {med * 1e3:.1f} ms/rep, single thread pinned to core {core}",
         "cpu_model": cpu_model(),
         "host_cpus": os.cpu_count(),
         "allowed_cpus": len(allowed),
     }
     return single, multicore
+
+
+def _core_ranges(cores) -> str:
+    """[0,1,2,5] -> '0-2,5'"""
+    out, start, prev = [], None, None
+    for c in sorted(cores):
+        if start is None:
+            start = prev = c
+        elif c == prev + 1:
+            prev = c
+        else:
+            out.append(f"{start}-{prev}" if prev != start else str(start))
+            start = prev = c
+    if start is not None:
+        out.append(f"{start}-{prev}" if prev != start else str(start))
+    return ",".join(out)
 
 
 def check_output(y, n, k, C, dt, seed, rank, samples=64, span=4096):
@@ -315,6 +393,10 @@ def run_workload(args, name, rank, world, with_cpu):
             "kernel_min_ms": round(min(kern_ms), 4),
             "kernel_median_ms": round(statistics.median(kern_ms), 4),
             "algorithmic_bytes_per_launch": alg_bytes,
+            "statistic": "mean of the per-launch HIP-event durations of the timed steps",
+            "scope": ("one launch over the whole signal" if world == 1 else
+                      "the interior launch of this rank's shard (frames >= head_frames); the halo wait and "
+                      "the head launch are outside it and only in value / ms_per_step"),
         },
     }
     if args.check:
@@ -355,6 +437,8 @@ def run_workload(args, name, rank, world, with_cpu):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(sys.argv[1:], args.gpus))
     rank, world, _ = init_dist(args)
     line = run_workload(args, args.workload, rank, world, with_cpu=True)
     if rank == 0:

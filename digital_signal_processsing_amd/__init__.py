@@ -58,6 +58,14 @@ def _algo_code(algo) -> int:
         raise ValueError(f"unknown algo {algo!r}; one of {sorted(ALGOS)}") from None
 
 
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
 def _stream_handle(stream, device) -> int:
     torch = _torch()
     if stream is None:
@@ -125,9 +133,12 @@ def moving_average_into(x, out, grade: int, channels: int = 1, algo="auto", hist
             # before the capture ends; pass one that outlives the graph
             raise ValueError(f"grade={grade} uses the look-back scan, which needs a {ws_n}-byte workspace: "
                              "inside a graph capture pass workspace= (see workspace_bytes())")
-        ws = torch.empty(ws_n, dtype=torch.uint8, device=x.device)
-        if stream is not None and stream != torch.cuda.current_stream(x.device):
-            ws.record_stream(stream)
+        # allocated on the launch stream itself: a block the caching allocator
+        # hands out there is free with respect to that stream's pending work
+        # (one taken on another stream could still be in use by kernels queued
+        # there, and record_stream only protects the free)
+        with torch.cuda.stream(stream) if stream is not None else _nullctx():
+            ws = torch.empty(ws_n, dtype=torch.uint8, device=x.device)
     st = _lib.load().mavg_run(x.data_ptr(), out.data_ptr(), x.numel(), channels, grade, dt,
                               _algo_code(algo), block_size, hist_ptr,
                               ws.data_ptr() if ws is not None else None, ws_n,
@@ -139,6 +150,15 @@ def moving_average(x, grade: int, channels: int = 1, algo="auto", history=None,
                    block_size: int = 0, stream=None):
     """Causal ``grade``-frame moving average of an interleaved signal ``x``."""
     torch = _torch()
+    if stream is not None and stream != torch.cuda.current_stream(x.device):
+        # x (and history) come from the caller's current stream: the launch
+        # stream waits for it, and `out` is allocated on the launch stream
+        stream.wait_stream(torch.cuda.current_stream(x.device))
+        with torch.cuda.stream(stream):
+            out = torch.empty_like(x)
+        moving_average_into(x, out, grade, channels, algo, history, block_size, stream)
+        x.record_stream(stream)
+        return out
     out = torch.empty_like(x)
     moving_average_into(x, out, grade, channels, algo, history, block_size, stream)
     return out

@@ -48,6 +48,12 @@ def _load():
     lib.oracle_synth_f32.argtypes = [p, sz, u64, u64, i]
     for f in (lib.oracle_mavg_i16, lib.oracle_mavg_f32, lib.oracle_window_sum_i64):
         f.restype = ctypes.c_int
+    pu = ctypes.POINTER(ctypes.c_uint64)
+    pd = ctypes.POINTER(ctypes.c_double)
+    lib.oracle_check_synth_f32.argtypes = [p, sz, i, i, u64, u64, i, ctypes.c_double, i, pu, pu, pd]
+    lib.oracle_check_synth_f32.restype = ctypes.c_int
+    lib.oracle_check_synth_i16.argtypes = [p, sz, i, i, u64, u64, i, pu, pu]
+    lib.oracle_check_synth_i16.restype = ctypes.c_int
     lib.oracle_synth_i16.restype = None
     lib.oracle_synth_f32.restype = None
     _lib = lib
@@ -134,3 +140,32 @@ def numpy_mavg_i16(x: np.ndarray, k: int, channels: int = 1) -> np.ndarray:
 
 def numpy_mavg_f32(x: np.ndarray, k: int, channels: int = 1) -> np.ndarray:
     return (numpy_window_sum(x.astype(np.float32), k, channels) / float(k)).astype(np.float32)
+
+
+def check_synth(y: np.ndarray, k: int, channels: int = 1, seed: int = 0x5EED, offset: int = 0, dist: int = 0,
+                rtol: float = 1e-5, threads: int = 0) -> dict:
+    """Check EVERY sample of a device output ``y`` against the restatement over
+    the counter-based synthetic stream (samples [offset, offset + y.size) of
+    it, zero history before sample 0) without materialising the input: int16
+    bit-exact, fp32 within ``rtol`` relative.  Chunked over ``threads`` cores;
+    exact for these inputs (see oracle_check_synth_f32 in mavg_oracle.c).
+    Returns {"checked", "mismatches", "first_bad" (sample index or None),
+    "max_rel" (fp32)}."""
+    threads = threads or min(16, len(os.sched_getaffinity(0)))
+    y = np.ascontiguousarray(y)
+    bad, first = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    if y.dtype == np.int16:
+        rc = _load().oracle_check_synth_i16(_ptr(y), y.size, channels, k, seed, offset, threads,
+                                            ctypes.byref(bad), ctypes.byref(first))
+        worst = None
+    elif y.dtype == np.float32:
+        mr = ctypes.c_double(0.0)
+        rc = _load().oracle_check_synth_f32(_ptr(y), y.size, channels, k, seed, offset, dist, rtol, threads,
+                                            ctypes.byref(bad), ctypes.byref(first), ctypes.byref(mr))
+        worst = mr.value
+    else:
+        raise TypeError(f"check_synth: int16 or float32 output, got {y.dtype}")
+    if rc != 0:
+        raise ValueError(f"oracle_check_synth: bad arguments (n={y.size}, C={channels}, k={k}, offset={offset})")
+    return {"checked": int(y.size), "mismatches": int(bad.value),
+            "first_bad": None if bad.value == 0 else int(first.value), "max_rel": worst}

@@ -28,6 +28,7 @@
 #include <stddef.h>
 #include <string.h>
 #include <stdlib.h>
+#include <math.h>
 
 #define ORACLE_MAX_CH 64
 
@@ -165,5 +166,103 @@ int oracle_mavg_f32_mt(const float* x, float* y, size_t n, int C, int k, int thr
                 y[i * C + ch] = (float)(sum[ch] / dk);
             }
     }
+    return 0;
+}
+
+/* ---- full-signal checkers over the synthetic stream ------------------------
+ * Compare a device output y (frames [g0, g0 + n/C) of the global counter-based
+ * stream, g0 = offset / C, zero history before global frame 0) against the
+ * restatement above WITHOUT materialising x: each sample is regenerated from
+ * its counter.  The frames are split into `threads` contiguous chunks, each
+ * seeded with the window sum of the k-1 frames before it.  This equals the
+ * serial loop (oracle_mavg_f32 / oracle_mavg_i16) exactly: int16 sums are
+ * integers, and every fp64 partial sum of dist-0 (int16-valued) or dist-1
+ * (multiples of 2^-24 below 1) samples is a multiple of 2^-24 below 2^29 in
+ * magnitude for k < 2^29, so fp64 adds them without rounding in any order.
+ * Used by the -m gpu full-size parity tests (every output of a 2^30 launch). */
+static inline float synth_f32_at(uint64_t seed, uint64_t i, int dist)
+{
+    uint64_t h = splitmix64(seed + i);
+    return dist == 1 ? (float)(h >> 40) * (1.0f / 16777216.0f) : (float)(int16_t)(uint16_t)(h >> 48);
+}
+
+int oracle_check_synth_f32(const float* y, size_t n, int C, int k, uint64_t seed, uint64_t offset,
+                           int dist, double rtol, int threads,
+                           uint64_t* n_bad, uint64_t* first_bad, double* max_rel)
+{
+    if (C < 1 || C > ORACLE_MAX_CH || k < 1 || k >= (1 << 29) || (n % (size_t)C) != 0 ||
+        (offset % (uint64_t)C) != 0 || threads < 1 || (dist != 0 && dist != 1))
+        return -1;
+    const size_t frames = n / (size_t)C;
+    const uint64_t g0 = offset / (uint64_t)C;
+    const double dk = (double)k;
+    uint64_t bad_total = 0, first = UINT64_MAX;
+    double worst = 0.0;
+#pragma omp parallel for num_threads(threads) schedule(static) reduction(+ : bad_total) \
+    reduction(min : first) reduction(max : worst)
+    for (int t = 0; t < threads; ++t) {
+        const size_t f0 = frames * (size_t)t / (size_t)threads;
+        const size_t f1 = frames * (size_t)(t + 1) / (size_t)threads;
+        for (int ch = 0; ch < C; ++ch) {
+            /* window sum of the k global frames [g-k, g-1] before g = g0 + f0:
+             * the first step below adds frame g and subtracts frame g-k */
+            const uint64_t g = g0 + f0;
+            const uint64_t lo = g >= (uint64_t)k ? g - (uint64_t)k : 0;
+            double s = 0.0;
+            for (uint64_t j = lo; j < g; ++j) s += (double)synth_f32_at(seed, j * C + ch, dist);
+            for (size_t f = f0; f < f1; ++f) {
+                const uint64_t gf = g0 + f;
+                s += (double)synth_f32_at(seed, gf * C + ch, dist);
+                if (gf >= (uint64_t)k) s -= (double)synth_f32_at(seed, (gf - k) * C + ch, dist);
+                const double want = (double)(float)(s / dk);
+                const double got = (double)y[f * C + ch];
+                const double err = fabs(got - want);
+                const double den = fabs(want) > 1e-30 ? fabs(want) : 1e-30;
+                const double rel = err / den;
+                if (!(err <= rtol * den)) {   /* NaN-safe */
+                    ++bad_total;
+                    if ((uint64_t)(f * C + ch) < first) first = (uint64_t)(f * C + ch);
+                }
+                if (rel > worst || rel != rel) worst = rel != rel ? INFINITY : rel;
+            }
+        }
+    }
+    *n_bad = bad_total;
+    *first_bad = first;
+    *max_rel = worst;
+    return 0;
+}
+
+int oracle_check_synth_i16(const int16_t* y, size_t n, int C, int k, uint64_t seed, uint64_t offset,
+                           int threads, uint64_t* n_bad, uint64_t* first_bad)
+{
+    if (C < 1 || C > ORACLE_MAX_CH || k < 1 || (n % (size_t)C) != 0 || (offset % (uint64_t)C) != 0 ||
+        threads < 1)
+        return -1;
+    const size_t frames = n / (size_t)C;
+    const uint64_t g0 = offset / (uint64_t)C;
+    uint64_t bad_total = 0, first = UINT64_MAX;
+#pragma omp parallel for num_threads(threads) schedule(static) reduction(+ : bad_total) reduction(min : first)
+    for (int t = 0; t < threads; ++t) {
+        const size_t f0 = frames * (size_t)t / (size_t)threads;
+        const size_t f1 = frames * (size_t)(t + 1) / (size_t)threads;
+        for (int ch = 0; ch < C; ++ch) {
+            const uint64_t g = g0 + f0;
+            const uint64_t lo = g >= (uint64_t)k ? g - (uint64_t)k : 0;
+            int64_t s = 0;
+            for (uint64_t j = lo; j < g; ++j) s += (int16_t)(uint16_t)(splitmix64(seed + j * C + ch) >> 48);
+            for (size_t f = f0; f < f1; ++f) {
+                const uint64_t gf = g0 + f;
+                s += (int16_t)(uint16_t)(splitmix64(seed + gf * C + ch) >> 48);
+                if (gf >= (uint64_t)k) s -= (int16_t)(uint16_t)(splitmix64(seed + (gf - k) * C + ch) >> 48);
+                if (y[f * C + ch] != (int16_t)(s / k)) {
+                    ++bad_total;
+                    if ((uint64_t)(f * C + ch) < first) first = (uint64_t)(f * C + ch);
+                }
+            }
+        }
+    }
+    *n_bad = bad_total;
+    *first_bad = first;
     return 0;
 }

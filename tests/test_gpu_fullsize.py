@@ -1,0 +1,68 @@
+"""Full-size parity: EVERY output of the BASELINE.json configurations (and the
+long-window / int16 bench lines) against the CPU restatement of
+basics/profilable_moving_averager.cpp:14-37, not samples of it.
+
+The input is the device counter-based generator; the oracle
+regenerates each sample from its counter (oracle.check_synth), so a 2^30
+launch is checked in a few seconds of host time without a host copy of x.
+fp32: within RTOL = 1e-5 relative (north_star); int16: bit-exact."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+SEED = 0x5EED
+
+CONFIGS = [
+    # id, samples, k, C, dtype, algo
+    ("headline_2p30_k1024", 1 << 30, 1024, 1, "f32", "blelloch"),   # BASELINE metric config (configs[4] per GPU)
+    ("config2_2p26_k64", 1 << 26, 64, 1, "f32", "blelloch"),        # configs[1]
+    ("config3_2p28_k7_direct", 1 << 28, 7, 1, "f32", "direct"),     # configs[2]
+    ("config4_2p30_k4096", 1 << 30, 4096, 1, "f32", "blelloch"),    # configs[3]
+    ("long_2p30_k44100", 1 << 30, 44100, 1, "f32", "blelloch"),     # look-ahead scan
+    ("hillis_2p30_k1024", 1 << 30, 1024, 1, "f32", "hillis"),
+    ("i16_2p30_k1024", 1 << 30, 1024, 1, "i16", "blelloch"),
+    ("i16_stereo_2p30_k44100", 1 << 30, 44100, 2, "i16", "blelloch"),  # 1 s windows on 44.1 kHz stereo PCM
+]
+
+
+@pytest.mark.parametrize("name,n,k,C,dt,algo", CONFIGS, ids=[c[0] for c in CONFIGS])
+def test_every_output_matches_oracle(oracle_mod, gpu, name, n, k, C, dt, algo):
+    import torch
+    import digital_signal_processsing_amd as dsp
+    dtype = torch.float32 if dt == "f32" else torch.int16
+    x = dsp.fill_synthetic(n, dtype, seed=SEED, device=gpu)
+    y = dsp.moving_average(x, k, channels=C, algo=algo)
+    del x
+    yh = y.cpu().numpy()
+    del y
+    r = oracle_mod.check_synth(yh, k, C, seed=SEED, rtol=RTOL)
+    assert r["checked"] == n
+    assert r["mismatches"] == 0, f"{name}: {r}"
+    if dt == "f32":
+        # int16-valued input: every window sum is exact in fp64, so the output
+        # is the correctly rounded quotient -- bit-equal, not merely 1e-5
+        assert r["max_rel"] == 0.0, f"{name}: {r}"
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_every_output_of_sharded_weak_scaling_signal(oracle_mod, gpu, world):
+    """BASELINE config #5 on one GPU: the 2^30-sample shards of a world*2^30
+    signal (what rank r holds under weak scaling, bench.py) filtered as
+    interior + head launch with rank r-1's tail as history; every output of
+    the first and a later shard is checked at its global offset."""
+    import torch
+    import digital_signal_processsing_amd as dsp
+    from digital_signal_processsing_amd.shard import split_moving_average_into
+    n, k = 1 << 30, 1024
+    for r in (0, world - 1):
+        x = dsp.fill_synthetic(n, torch.float32, seed=SEED, offset=r * n, device=gpu)
+        hist = (dsp.fill_synthetic(k - 1, torch.float32, seed=SEED, offset=r * n - (k - 1), device=gpu)
+                if r > 0 else None)
+        y = torch.empty_like(x)
+        split_moving_average_into(x, y, k, 1, "blelloch", history=hist)
+        del x
+        res = oracle_mod.check_synth(y.cpu().numpy(), k, 1, seed=SEED, offset=r * n, rtol=RTOL)
+        del y
+        assert res["mismatches"] == 0 and res["max_rel"] == 0.0, f"rank {r}/{world}: {res}"

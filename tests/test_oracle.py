@@ -112,3 +112,36 @@ def test_multicore_baseline_equals_serial(oracle_mod, C, k, threads):
     x = oracle_mod.synth_f32(200_003 * C, offset=k, dist=1)
     np.testing.assert_allclose(oracle_mod.mavg_f32_mt(x, k, C, threads), oracle_mod.mavg_f32(x, k, C),
                                rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("C,k,dist,offset,threads", [
+    (1, 1024, 0, 0, 7), (2, 41, 1, 0, 3), (1, 7, 0, 12345, 8), (3, 300, 1, 99 * 3, 5), (1, 5000, 0, 0, 1),
+    (2, 1, 0, 2, 4), (1, 70_000, 0, 4096, 6)])
+def test_full_signal_checker_equals_serial_loop(oracle_mod, C, k, dist, offset, threads):
+    """check_synth (chunked, x regenerated from its counter) accepts exactly
+    the serial restatement's output, at any offset into the stream, and
+    reports the first corrupted sample."""
+    n = 150_001 * C
+    x = oracle_mod.synth_f32(n + offset, dist=dist)
+    y = oracle_mod.mavg_f32(x, k, C)[offset:]
+    r = oracle_mod.check_synth(y, k, C, offset=offset, dist=dist, threads=threads)
+    assert r["mismatches"] == 0 and r["checked"] == n and r["max_rel"] == 0.0, r
+    y[n // 3] = np.nextafter(y[n // 3], np.float32(np.inf)) * np.float32(1.0001)
+    r = oracle_mod.check_synth(y, k, C, offset=offset, dist=dist, threads=threads)
+    assert r["mismatches"] == 1 and r["first_bad"] == n // 3, r
+    xi = oracle_mod.synth_i16(n + offset)
+    yi = oracle_mod.mavg_i16(xi, k, C)[offset:]
+    assert oracle_mod.check_synth(yi, k, C, offset=offset, threads=threads)["mismatches"] == 0
+    yi[0] ^= 1
+    yi[-1] ^= 1
+    r = oracle_mod.check_synth(yi, k, C, offset=offset, threads=threads)
+    assert r["mismatches"] == 2 and r["first_bad"] == 0, r
+
+
+def test_full_signal_checker_rejects_bad_args(oracle_mod):
+    y = np.zeros(10, np.float32)
+    for kw in (dict(k=0), dict(k=3, channels=3), dict(k=3, channels=2, offset=1), dict(k=3, dist=2)):
+        with pytest.raises(ValueError):
+            oracle_mod.check_synth(y, **kw)
+    with pytest.raises(TypeError):
+        oracle_mod.check_synth(np.zeros(4, np.float64), 3)

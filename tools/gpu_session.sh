@@ -40,6 +40,12 @@ for step in "$@"; do
             --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --check &&
           run dist4 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
             --master-port 29512 bench.py --gpus 4 --steps 3 --warmup 1 --dist-backend gloo --check ;;
+    full) run pytest_full 900 python -u -m pytest tests/test_gpu_fullsize.py tests/test_bench_launch.py -m gpu -x -v \
+            --timeout 170 --timeout-method thread -p no:cacheprovider ;;
+    # the driver's exact bench command, then the same command under the kernel tracer
+    drv) run drv_bench 400 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    drvprof) run drv_prof 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/drvprof" -o run -- \
+            python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     *) echo "unknown step $step" ;;
   esac
 done
