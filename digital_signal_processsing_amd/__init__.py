@@ -73,10 +73,11 @@ def _stream_handle(stream, device) -> int:
     return stream.cuda_stream
 
 
-def workspace_bytes(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto") -> int:
+def workspace_bytes(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto",
+                    block_size: int = 0) -> int:
     import ctypes
     out = ctypes.c_size_t(0)
-    _lib.check(_lib.load().mavg_workspace_bytes(n, channels, grade, dtype, _algo_code(algo), 0,
+    _lib.check(_lib.load().mavg_workspace_bytes(n, channels, grade, dtype, _algo_code(algo), block_size,
                                                 ctypes.byref(out)), "mavg_workspace_bytes")
     return out.value
 
@@ -85,11 +86,12 @@ def resolve_algo(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="
     return algo_name(_lib.load().mavg_resolve_algo(n, channels, grade, dtype, _algo_code(algo)))
 
 
-def plan(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto") -> str:
+def plan(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto", block_size: int = 0) -> str:
     """The kernel and launch geometry mavg_run would use (nothing is launched)."""
     import ctypes
     buf = ctypes.create_string_buffer(256)
-    _lib.check(_lib.load().mavg_plan(n, channels, grade, dtype, _algo_code(algo), buf, len(buf)), "mavg_plan")
+    _lib.check(_lib.load().mavg_plan(n, channels, grade, dtype, _algo_code(algo), block_size, buf, len(buf)),
+               "mavg_plan")
     return buf.value.decode()
 
 
@@ -118,7 +120,7 @@ def moving_average_into(x, out, grade: int, channels: int = 1, algo="auto", hist
         hist_ptr = history.data_ptr() if history.numel() else None
     # workspace (look-back scan only): from torch's caching allocator, tied to
     # the launch stream so it is not handed out again before the kernel ends
-    ws_n = workspace_bytes(x.numel(), grade, channels, dt, algo)
+    ws_n = workspace_bytes(x.numel(), grade, channels, dt, algo, block_size)
     ws = None
     if ws_n and workspace is not None:
         if not (workspace.is_cuda and workspace.is_contiguous()):

@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "mavg_strerror",
     "mavg_algo_name",
     "mavg_abi_version",
+    "mavg_test_ahead_schedule",
 )
 
 
@@ -93,7 +94,7 @@ def load() -> ctypes.CDLL:
     lib.mavg_run.restype = i
     lib.mavg_resolve_algo.argtypes = [sz, i, i, i, i]
     lib.mavg_resolve_algo.restype = i
-    lib.mavg_plan.argtypes = [sz, i, i, i, i, ctypes.c_char_p, sz]
+    lib.mavg_plan.argtypes = [sz, i, i, i, i, i, ctypes.c_char_p, sz]
     lib.mavg_plan.restype = i
     lib.mavg_fill_synthetic.argtypes = [vp, sz, i, u64, u64, i, vp]
     lib.mavg_fill_synthetic.restype = i
@@ -103,6 +104,8 @@ def load() -> ctypes.CDLL:
     lib.mavg_algo_name.restype = ctypes.c_char_p
     lib.mavg_stream_copy.argtypes = [vp, vp, sz, vp]
     lib.mavg_stream_copy.restype = i
+    lib.mavg_test_ahead_schedule.argtypes = [i, i]
+    lib.mavg_test_ahead_schedule.restype = i
     lib.mavg_abi_version.argtypes = []
     lib.mavg_abi_version.restype = i
     _lib = lib

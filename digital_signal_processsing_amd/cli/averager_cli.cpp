@@ -201,6 +201,11 @@ int run_gpu(const Options& o, int C, const std::vector<int16_t>& samples, std::v
     std::cout << "point: " << o.grade << std::endl;
     std::cout << "block Size: " << o.block << std::endl;
   }
+  {  // the launch the block size maps to (workgroup = the next power of two >= 64, see mavg.h)
+    char plan[512] = {0};
+    if (n > 0) MAVG_CHECK(mavg_plan(n, C, o.grade, MAVG_I16, kV.algo, o.block, plan, sizeof(plan)));
+    std::cout << "Kernel: " << plan << std::endl;
+  }
   if (o.standard) {
     std::cout << "\n--- MEM MODE: STANDARD (Discrete) ---" << std::endl;
     profile_mode<MemoryMode::Standard>(o, C, n, samples, out, logger);
@@ -291,7 +296,7 @@ int run_gpu_synthetic(const Options& o) {
   const size_t n = o.synth_n / (size_t)C * (size_t)C;
   CsvLogger logger(o.csv);
   char plan[512] = {0};
-  MAVG_CHECK(mavg_plan(n, C, o.grade, o.dtype, kV.algo, plan, sizeof(plan)));
+  MAVG_CHECK(mavg_plan(n, C, o.grade, o.dtype, kV.algo, o.block, plan, sizeof(plan)));
   std::cout << "--- SYNTHETIC " << dtype_name(o.dtype) << " (" << kV.csv_name << ") ---" << std::endl;
   std::cout << "Samples: " << n << "  channels: " << C << "  point: " << o.grade << "  block Size: " << o.block
             << std::endl;

@@ -18,8 +18,8 @@ bin_cpu's on the same WAV (all variants are bit-exact on int16).
 WAV sweep: #1-#4 through the bin_* programs' synthetic fp32
 mode (HBM-resident input, kernel-only timing, roofline line), #5 -- the
 sharded signal, 2^30 samples per GPU, k=1024, (k-1)-sample RCCL halo --
-through bench.py under torch.distributed.run at 1, 2, 4 and 8 GPUs, as many
-as the node has.
+through bench.py --gpus N (which starts one rank per GPU) at 1, 2, 4 and 8
+GPUs, as many as the node has.
 
     cd digital_signal_processsing_amd/cli && python run_benchmarks.py --quick
     python run_benchmarks.py --baseline-configs --verify
@@ -211,11 +211,7 @@ def run_baseline_configs(configs, verify=False, max_gpus=None, timeout=900) -> i
         for g in [g for g in SHARDED_GPUS if g <= have]:
             bench = [os.path.join(REPO, "bench.py"), "--gpus", str(g), "--steps", "20", "--warmup", "5",
                      "--no-cpu-baseline"] + (["--check"] if verify else [])
-            if g == 1:
-                cmd = [sys.executable] + bench
-            else:
-                cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={g}",
-                       "--master-addr", "127.0.0.1", "--master-port", str(29600 + g)] + bench
+            cmd = [sys.executable] + bench  # bench.py --gpus g starts its g ranks itself
             label = f"sharded signal, {g} x 2^30 fp32, k=1024, RCCL halo"
             print(f"== config #5 ({g} GPU): {' '.join(cmd)}", flush=True)
             r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, universal_newlines=True,

@@ -5,6 +5,8 @@
 namespace mavg {
 
 thread_local LaunchPlan* g_plan = nullptr;
+std::atomic<int> g_test_ahead_slots{-1};
+std::atomic<int> g_test_ahead_spin{-1};
 
 // ---- per-device attribute cache (no stream work, capture-safe) --------------
 constexpr int kMaxDevices = 64;
@@ -40,3 +42,9 @@ OutParams make_out_params(int k) {
 }
 
 }  // namespace mavg
+
+extern "C" int mavg_test_ahead_schedule(int slots, int spin) {
+  mavg::g_test_ahead_slots.store(slots < 0 ? -1 : std::min(slots, 1 << 30), std::memory_order_relaxed);
+  mavg::g_test_ahead_spin.store(spin < 0 ? -1 : std::min(spin, 1 << 20), std::memory_order_relaxed);
+  return MAVG_OK;
+}

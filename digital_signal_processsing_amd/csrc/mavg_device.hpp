@@ -145,6 +145,32 @@ struct UnitIO {
     }
     return u;
   }
+  // Global-memory forms.  eio (uniform): the pointer is only element-aligned
+  // (a frame-unit launch on a misaligned view, mavg_api.hip), so a
+  // multi-element unit moves as element accesses instead of one vector access.
+  template <bool NT = false>
+  __device__ __forceinline__ static Unit<T, VE> gload(const T* __restrict__ p, bool eio) {
+    if constexpr (kVec && VE > 1) {
+      if (eio) {
+        Unit<T, VE> u;
+#pragma unroll
+        for (int i = 0; i < VE; ++i) u.e[i] = p[i];
+        return u;
+      }
+    }
+    return load<NT>(p);
+  }
+  template <bool NT = false>
+  __device__ __forceinline__ static void gstore(T* __restrict__ p, const Unit<T, VE>& u, bool eio) {
+    if constexpr (kVec && VE > 1) {
+      if (eio) {
+#pragma unroll
+        for (int i = 0; i < VE; ++i) p[i] = u.e[i];
+        return;
+      }
+    }
+    store<NT>(p, u);
+  }
   template <bool NT = false>
   __device__ __forceinline__ static void store(T* __restrict__ p, const Unit<T, VE>& u) {
     if constexpr (kVec) {
@@ -187,12 +213,15 @@ __device__ __forceinline__ Unit<T, VE> extract(const Unit<T, VE>& a, const Unit<
 // ----------------------------------------------------------------------------
 // guarded element access: frames < 0 come from the history (the multi-GPU
 // halo / the reference's zero halo, gpu_utils.h:112-123), frames >= nframes
-// and frames before the history read as zero.
+// and frames before the history read as zero.  `pre` > 0 (the body launch
+// after a peeled misaligned head, mavg_api.hip): frames [-pre, 0) are the
+// head, readable in front of `in`, and only frames before -pre come from
+// `hist` (which the host then offsets by pre frames).
 // ----------------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ T load_elem(const T* __restrict__ in, const T* __restrict__ hist,
-                                       long long f, int c, int C, long long nframes, int k) {
-  if (f >= 0) return f < nframes ? in[f * C + c] : (T)0;
+                                       long long f, int c, int C, long long nframes, int k, int pre) {
+  if (f >= -(long long)pre) return f < nframes ? in[f * C + c] : (T)0;
   if (hist != nullptr && f >= -(long long)(k - 1)) return hist[(f + (k - 1)) * C + c];
   return (T)0;
 }

@@ -26,6 +26,8 @@ struct DirectParams {
   int m;          // ceil((k-1)/F): halo units in front of every lane's own unit
   int off;        // m*F - (k-1): first window frame inside the first covering unit
   int xcd_remap;
+  int pre;        // frames in front of `in` that are readable signal (load_elem)
+  int eio;        // frame-unit launch on element-aligned pointers (UnitIO::gload)
   OutParams o;
 };
 
@@ -77,6 +79,8 @@ __global__ __launch_bounds__(WG) void direct_kernel(DirectParams p) {
   const int k = p.k;
   const int m = p.m;
   const long long nframes = p.nframes;
+  const int pre = p.pre;
+  const bool eio = F == 1 && p.eio != 0;
 
   const long long tile = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
   const long long t0 = tile * TF;
@@ -88,12 +92,12 @@ __global__ __launch_bounds__(WG) void direct_kernel(DirectParams p) {
   for (int u = 0; u < U; ++u) {
     const long long f = t0 + (long long)(u * WG + tid) * F;
     if (tile_full) {
-      xr[u] = IO::load(in + f * C);
+      xr[u] = IO::gload(in + f * C, eio);
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-        for (int c = 0; c < C; ++c) xr[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+        for (int c = 0; c < C; ++c) xr[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k, pre);
     }
   }
   const bool halo_fast = h0 >= 0;
@@ -101,12 +105,12 @@ __global__ __launch_bounds__(WG) void direct_kernel(DirectParams p) {
     const long long f = h0 + (long long)j * F;
     U_t h;
     if (halo_fast) {
-      h = IO::load(in + f * C);
+      h = IO::gload(in + f * C, eio);
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-        for (int c = 0; c < C; ++c) h.e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+        for (int c = 0; c < C; ++c) h.e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k, pre);
     }
     IO::store(stage + j * VE, h);
   }
@@ -177,7 +181,7 @@ __global__ __launch_bounds__(WG) void direct_kernel(DirectParams p) {
 #pragma unroll
       for (int c = 0; c < C; ++c) y.e[fr * C + c] = to_out<T, A>(wsum[fr][c], p.o);
     if (tile_full) {
-      IO::store(out + f * C, y);
+      IO::gstore(out + f * C, y, eio);
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)

@@ -42,6 +42,30 @@ template <> constexpr const char* type_name<double>() { return "f64"; }
 template <> constexpr const char* type_name<int32_t>() { return "i32"; }
 template <> constexpr const char* type_name<int64_t>() { return "i64"; }
 
+// One launch's view of the signal: caller-owned device pointers, the frame
+// count, and two properties of a view the kernels must respect:
+//   pre  frames in front of `in` that are readable signal: the body launch
+//        after a peeled misaligned head (mavg_api.hip); `hist` then holds the
+//        frames before those (load_elem)
+//   eio  the pointers are only element-aligned: a frame-unit (F = 1) launch
+//        moves multi-element frames as element accesses (UnitIO::gload)
+struct Sig {
+  const void* in;
+  void* out;
+  const void* hist;
+  long long nframes;
+  int pre = 0;
+  int eio = 0;
+};
+
+// Workgroup size a non-zero reference block size (argv; a multiple of 32 in
+// [32, 1024]) maps to: the next power of two, at least one wave64.
+constexpr int block_wg(int block) {
+  int wg = 64;
+  while (wg < block && wg < 1024) wg <<= 1;
+  return wg;
+}
+
 // family entry points (defined in mavg_scan_*.hip / mavg_direct.hip)
 // Workspace: the look-ahead scan needs its record granules (ahead_granule_bytes)
 // in caller-owned device memory (zeroed on the stream before each launch);
@@ -50,16 +74,12 @@ struct Workspace {
   void* ptr = nullptr;
   size_t bytes = 0;
 };
-int scan_f32(int C, bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes, int k,
-             hipStream_t st, Workspace ws);
-int scan_i16(int C, bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes, int k,
-             hipStream_t st, Workspace ws);
-int scan_i16_wide(int C, bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes,
-                  int k, hipStream_t st, Workspace ws);
-int direct_any(int dtype, bool wide, int C, int width, const void* in, void* out, const void* hist,
-               long long nframes, int k, hipStream_t st);
-int naive_any(int dtype, bool wide, const void* in, void* out, const void* hist, long long nframes, int C, int k,
-              hipStream_t st);
+// block: the reference's block size (0 = the tuned geometry)
+int scan_f32(int C, bool vec, bool hs, const Sig& sg, int k, int block, hipStream_t st, Workspace ws);
+int scan_i16(int C, bool vec, bool hs, const Sig& sg, int k, int block, hipStream_t st, Workspace ws);
+int scan_i16_wide(int C, bool vec, bool hs, const Sig& sg, int k, int block, hipStream_t st, Workspace ws);
+int direct_any(int dtype, bool wide, int C, int width, const Sig& sg, int k, int block, hipStream_t st);
+int naive_any(int dtype, bool wide, const Sig& sg, int C, int k, int block, hipStream_t st);
 
 // ---- streaming scan launch ----------------------------------------------------
 // Launch geometry knobs (tuned on MI355X with tools/tune).
@@ -71,16 +91,18 @@ struct ScanTuning {
 };
 
 template <typename T, typename A, int C, int F, int U, bool HS, int PD = 1, int NT = 0>
-int launch_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
-                ScanTuning tune = ScanTuning()) {
+int launch_scan(const Sig& sg, int k, hipStream_t st, ScanTuning tune = ScanTuning()) {
   constexpr int CHF = kWG * F * U;
   constexpr int NSEG = U * kNW;
   constexpr int VE = F * C;
+  const long long nframes = sg.nframes;
   ScanParams p{};
-  p.in = in;
-  p.out = out;
-  p.hist = hist;
+  p.in = sg.in;
+  p.out = sg.out;
+  p.hist = sg.hist;
   p.nframes = nframes;
+  p.pre = sg.pre;
+  p.eio = sg.eio;
   p.k = k;
   p.o = make_out_params(k);
   p.pre_chunks = (k - 1 + CHF - 1) / CHF;
@@ -122,16 +144,18 @@ int launch_scan(const void* in, void* out, const void* hist, long long nframes, 
 // flat-tile scan: one workgroup per tile, carry rebuilt from the k-frame halo
 template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, int WG = kWG,
           bool RC = true>
-int launch_tile_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
-                     int xcd_remap = kRemapGroup) {
+int launch_tile_scan(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
   constexpr int TF = WG * F * U;
   constexpr int NSEG = U * (WG / 64);
   constexpr int VE = F * C;
+  const long long nframes = sg.nframes;
   TileParams p{};
-  p.in = in;
-  p.out = out;
-  p.hist = hist;
+  p.in = sg.in;
+  p.out = sg.out;
+  p.hist = sg.hist;
   p.nframes = nframes;
+  p.pre = sg.pre;
+  p.eio = sg.eio;
   p.k = k;
   p.o = make_out_params(k);
   p.halo_units = (k + F - 1) / F;
@@ -171,15 +195,12 @@ int launch_tile_scan(const void* in, void* out, const void* hist, long long nfra
 // 16 bytes (the memset's fast form, cdna_hip_programming.md Guideline 16).
 constexpr int kAheadSlots = 512;  // D: dispatch slots between a record's producer and its tile (multiple of 8)
 constexpr int kAheadSpin = 256;   // polls of an untagged granule before recomputing it
-// Test knobs: MAVG_AHEAD_SLOTS / MAVG_AHEAD_SPIN override the two constants
-// (the parity tests force the recompute path with SPIN=0 and short or absent
-// look-ahead); results are bitwise the same for every setting.
-inline int ahead_knob(const char* name, int dflt, int lo, int hi) {
-  const char* v = getenv(name);
-  if (v == nullptr || *v == 0) return dflt;
-  const long x = strtol(v, nullptr, 10);
-  return (int)std::min<long>(hi, std::max<long>(lo, x));
-}
+// Test hook (mavg_test_ahead_schedule): the parity tests force the
+// recompute path with spin 0 and short or absent look-ahead; results are
+// bitwise the same for every setting.  -1 = the constants above.  Relaxed
+// atomics: no environment reads on the launch path.
+extern std::atomic<int> g_test_ahead_slots;
+extern std::atomic<int> g_test_ahead_spin;
 template <typename T, typename A, int C, int F, int U>
 constexpr size_t ahead_granule_bytes(long long nfull) {
   using SA = typename ScanAcc<T, A>::type;
@@ -188,10 +209,16 @@ constexpr size_t ahead_granule_bytes(long long nfull) {
 }
 template <typename T, typename A, int C, int F, int U, int NT = kNtStore, int ORD = 2, bool RC = false, int WPS = 1,
           int PF = 0>
-int launch_ahead_scan(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
-                      Workspace ws, int ahead = -1, int spin = -1) {
-  if (ahead < 0) ahead = ahead_knob("MAVG_AHEAD_SLOTS", kAheadSlots, 0, 1 << 30) & ~7;
-  if (spin < 0) spin = ahead_knob("MAVG_AHEAD_SPIN", kAheadSpin, 0, 1 << 20);
+int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead = -1, int spin = -1) {
+  const long long nframes = sg.nframes;
+  if (ahead < 0) {
+    const int t = g_test_ahead_slots.load(std::memory_order_relaxed);
+    ahead = (t >= 0 ? t : kAheadSlots) & ~7;
+  }
+  if (spin < 0) {
+    const int t = g_test_ahead_spin.load(std::memory_order_relaxed);
+    spin = t >= 0 ? t : kAheadSpin;
+  }
   constexpr int xcd_remap = 1;  // one run per XCD (see ahead_scan_kernel)
   constexpr int TF = kWG * F * U;
   constexpr int VE = F * C;
@@ -222,10 +249,12 @@ int launch_ahead_scan(const void* in, void* out, const void* hist, long long nfr
   if ((reinterpret_cast<uintptr_t>(ws.ptr) & 15u) != 0) return MAVG_ERR_MISALIGNED;
   if (hipMemsetAsync(ws.ptr, 0, need, st) != hipSuccess) return MAVG_ERR_HIP;
   AheadParams p{};
-  p.in = in;
-  p.out = out;
-  p.hist = hist;
+  p.in = sg.in;
+  p.out = sg.out;
+  p.hist = sg.hist;
   p.nframes = nframes;
+  p.pre = sg.pre;
+  p.eio = sg.eio;
   p.nfull = nfull;
   p.k = k;
   p.o = make_out_params(k);
@@ -250,13 +279,13 @@ int launch_ahead_scan(const void* in, void* out, const void* hist, long long nfr
 // XCD-remapped segments of at least 4 chunks and 4x the pre-roll (5.5-5.7
 // TB/s vs 5.0 for one long segment per workgroup, tools/tune/tune_scan.hip)
 template <typename T, typename A, int C, int F, bool HS>
-int launch_segment_rule(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st) {
+int launch_segment_rule(const Sig& sg, int k, hipStream_t st) {
   constexpr int SU = F >= 4 ? 2 : 8;
   constexpr int CHF = kWG * F * SU;
   ScanTuning t;
   t.xcd_remap = 1;
   t.seg_chunks = std::max(4, 4 * ((k - 1 + CHF - 1) / CHF));
-  return launch_scan<T, A, C, F, SU, HS, 2, 0>(in, out, hist, nframes, k, st, t);
+  return launch_scan<T, A, C, F, SU, HS, 2, 0>(sg, k, st, t);
 }
 // ... and whether its LDS ring holds the window (else it re-reads x[n-k]
 // from global memory, measured 0.25-0.40 of peak)
@@ -284,8 +313,7 @@ bool segment_ring_fits(int k) {
 //   for H <= 512 B, else U8 ntS; int16: U4 x 512 threads ntS), then the
 //   segment-streaming scan.
 template <typename T, typename A, int C, int F, bool HS>
-int dispatch_scan_f(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
-                    Workspace ws) {
+int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace ws) {
   constexpr int VE = F * C;
   constexpr int kUnitBytes = VE * (int)sizeof(T);
   const long long halo_bytes = (long long)k * C * (long long)sizeof(T);
@@ -300,6 +328,18 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
   // nt halo loads (their last use), nt stores (tools/tune/sweep_nt.sh: +1-4 %
   // over default-policy loads wherever the halo is re-read from L2)
   constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
+  if (block != 0) {
+    // the reference's block size: a U=2 tile of block_wg(block) threads while
+    // its halo fits that workgroup's LDS, else the tuned dispatch below (the
+    // plan string shows the workgroup that runs)
+    const int wg = block_wg(block);
+    constexpr bool kR = sizeof(T) == 4;  // RC as in the tuned rules (fp32 on, int16 off)
+    if (wg == 64 && fits(2, 64)) return launch_tile_scan<T, A, C, F, 2, HS, kNtS, 64, kR>(sg, k, st);
+    if (wg == 128 && fits(2, 128)) return launch_tile_scan<T, A, C, F, 2, HS, kNtS, 128, kR>(sg, k, st);
+    if (wg == 256 && fits(2, 256)) return launch_tile_scan<T, A, C, F, 2, HS, kNtS, 256, kR>(sg, k, st);
+    if (wg == 512 && fits(2, 512)) return launch_tile_scan<T, A, C, F, 2, HS, kNtS, 512, kR>(sg, k, st);
+    if (wg == 1024 && fits(2, 1024)) return launch_tile_scan<T, A, C, F, 2, HS, kNtS, 1024, kR>(sg, k, st);
+  }
   if constexpr (!HS) {
     // RC (in-lane prefix rebuilt after the barrier): on for fp32, off for
     // int16 (measured both ways, tools/tune/ab_rc.sh, sweep_lookback2.sh).
@@ -307,87 +347,87 @@ int dispatch_scan_f(const void* in, void* out, const void* hist, long long nfram
     // carries more waves (tools/tune/sweep_wg.sh, sweep_wg2.sh).
     if constexpr (sizeof(T) == 2) {
       if (halo_bytes <= 256 && fits(2, kWG))
-        return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, false>(sg, k, st);
       if (halo_bytes <= 4096 && fits(4, kWG))
-        return launch_tile_scan<T, A, C, F, 4, false, kNt, kWG, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 4, false, kNt, kWG, false>(sg, k, st);
       if (halo_bytes <= 8192 && fits(4, kWG))
-        return launch_tile_scan<T, A, C, F, 4, false, kNtS, kWG, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 4, false, kNtS, kWG, false>(sg, k, st);
       if (halo_bytes <= 16384 && fits(4, 512))
-        return launch_tile_scan<T, A, C, F, 4, false, kNtS, 512, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 4, false, kNtS, 512, false>(sg, k, st);
       if (fits(2, 1024))
-        return launch_tile_scan<T, A, C, F, 2, false, kNtS, 1024, false>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, kNtS, 1024, false>(sg, k, st);
     } else {
       if (C == 1 && halo_bytes <= 512 && fits(2, kWG))
-        return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, true>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, true>(sg, k, st);
       if (halo_bytes <= 4096 && fits(2, kWG))
-        return launch_tile_scan<T, A, C, F, 2, false, kNtS, kWG, true>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, kNtS, kWG, true>(sg, k, st);
       if (halo_bytes <= 8192 && fits(2, 512))
-        return launch_tile_scan<T, A, C, F, 2, false, kNtS, 512, true>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 2, false, kNtS, 512, true>(sg, k, st);
       if (halo_bytes <= 16384 && fits(4, 512))
-        return launch_tile_scan<T, A, C, F, 4, false, kNtS, 512, true>(in, out, hist, nframes, k, st);
+        return launch_tile_scan<T, A, C, F, 4, false, kNtS, 512, true>(sg, k, st);
       // fp32 halos past 16 KiB: the look-ahead scan beats the 1024-thread
       // tile (k=8192: 0.73 vs 0.69; k=12000: 0.71 vs 0.64, sweep_ahead.sh)
     }
-    return launch_ahead_scan<T, A, C, F, 4, kNtStore>(in, out, hist, nframes, k, st, ws);
+    return launch_ahead_scan<T, A, C, F, 4, kNtStore>(sg, k, st, ws);
   } else {
     // Hillis-Steele: the element-wise log-step scans make a tile's compute
     // long, so bigger tiles (fewer halos and barriers per byte) and the split
     // cache policy win (tools/tune/sweep_hillis.sh: fp32 k=1024 0.66 -> 0.78)
     if constexpr (sizeof(T) == 2) {
       if (fits(4, 512))
-        return launch_tile_scan<T, A, C, F, 4, HS, kNtS, 512>(in, out, hist, nframes, k, st, kRemapGroup);
+        return launch_tile_scan<T, A, C, F, 4, HS, kNtS, 512>(sg, k, st, kRemapGroup);
     } else {
       if (C == 1 && halo_bytes <= 512 && fits(4, kWG))
-        return launch_tile_scan<T, A, C, F, 4, HS, kNt>(in, out, hist, nframes, k, st, kRemapGroup);
+        return launch_tile_scan<T, A, C, F, 4, HS, kNt>(sg, k, st, kRemapGroup);
       if (fits(8, kWG))
-        return launch_tile_scan<T, A, C, F, 8, HS, kNtS>(in, out, hist, nframes, k, st, kRemapGroup);
+        return launch_tile_scan<T, A, C, F, 8, HS, kNtS>(sg, k, st, kRemapGroup);
     }
     (void)kB;
-    return launch_segment_rule<T, A, C, F, HS>(in, out, hist, nframes, k, st);
+    return launch_segment_rule<T, A, C, F, HS>(sg, k, st);
   }
 }
 
 template <typename T, typename A, int C>
-int dispatch_scan_c(bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes, int k,
-                    hipStream_t st, Workspace ws) {
+int dispatch_scan_c(bool vec, bool hs, const Sig& sg, int k, int block, hipStream_t st, Workspace ws) {
   constexpr int VF = (C * (int)sizeof(T) <= 16 && 16 % (C * (int)sizeof(T)) == 0) ? 16 / (C * (int)sizeof(T)) : 0;
   if constexpr (VF > 0) {
     if (vec) {
-      return hs ? dispatch_scan_f<T, A, C, VF, true>(in, out, hist, nframes, k, st, ws)
-                : dispatch_scan_f<T, A, C, VF, false>(in, out, hist, nframes, k, st, ws);
+      return hs ? dispatch_scan_f<T, A, C, VF, true>(sg, k, block, st, ws)
+                : dispatch_scan_f<T, A, C, VF, false>(sg, k, block, st, ws);
     }
   }
-  return hs ? dispatch_scan_f<T, A, C, 1, true>(in, out, hist, nframes, k, st, ws)
-            : dispatch_scan_f<T, A, C, 1, false>(in, out, hist, nframes, k, st, ws);
+  return hs ? dispatch_scan_f<T, A, C, 1, true>(sg, k, block, st, ws)
+            : dispatch_scan_f<T, A, C, 1, false>(sg, k, block, st, ws);
 }
 
 template <typename T, typename A>
-int dispatch_scan(int C, bool vec, bool hs, const void* in, void* out, const void* hist, long long nframes,
-                  int k, hipStream_t st, Workspace ws) {
+int dispatch_scan(int C, bool vec, bool hs, const Sig& sg, int k, int block, hipStream_t st, Workspace ws) {
   switch (C) {
-    case 1: return dispatch_scan_c<T, A, 1>(vec, hs, in, out, hist, nframes, k, st, ws);
-    case 2: return dispatch_scan_c<T, A, 2>(vec, hs, in, out, hist, nframes, k, st, ws);
-    case 3: return dispatch_scan_c<T, A, 3>(vec, hs, in, out, hist, nframes, k, st, ws);
-    case 4: return dispatch_scan_c<T, A, 4>(vec, hs, in, out, hist, nframes, k, st, ws);
-    case 5: return dispatch_scan_c<T, A, 5>(vec, hs, in, out, hist, nframes, k, st, ws);
-    case 6: return dispatch_scan_c<T, A, 6>(vec, hs, in, out, hist, nframes, k, st, ws);
-    case 7: return dispatch_scan_c<T, A, 7>(vec, hs, in, out, hist, nframes, k, st, ws);
-    case 8: return dispatch_scan_c<T, A, 8>(vec, hs, in, out, hist, nframes, k, st, ws);
+    case 1: return dispatch_scan_c<T, A, 1>(vec, hs, sg, k, block, st, ws);
+    case 2: return dispatch_scan_c<T, A, 2>(vec, hs, sg, k, block, st, ws);
+    case 3: return dispatch_scan_c<T, A, 3>(vec, hs, sg, k, block, st, ws);
+    case 4: return dispatch_scan_c<T, A, 4>(vec, hs, sg, k, block, st, ws);
+    case 5: return dispatch_scan_c<T, A, 5>(vec, hs, sg, k, block, st, ws);
+    case 6: return dispatch_scan_c<T, A, 6>(vec, hs, sg, k, block, st, ws);
+    case 7: return dispatch_scan_c<T, A, 7>(vec, hs, sg, k, block, st, ws);
+    case 8: return dispatch_scan_c<T, A, 8>(vec, hs, sg, k, block, st, ws);
     default: return MAVG_ERR_UNSUPPORTED;
   }
 }
 
 // ---- direct LDS-tiled launch ---------------------------------------------------
 template <typename T, typename A, int C, int F, int U = 1, int WG = kWG>
-int launch_direct(const void* in, void* out, const void* hist, long long nframes, int k, hipStream_t st,
-                  int xcd_remap = kRemapGroup) {
+int launch_direct(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
   constexpr int TF = WG * F * U;
   constexpr int VE = F * C;
+  const long long nframes = sg.nframes;
   DirectParams p{};
-  p.in = in;
-  p.out = out;
-  p.hist = hist;
+  p.in = sg.in;
+  p.out = sg.out;
+  p.hist = sg.hist;
   p.nframes = nframes;
+  p.pre = sg.pre;
+  p.eio = sg.eio;
   p.k = k;
   p.o = make_out_params(k);
   p.m = (k - 1 + F - 1) / F;
@@ -406,50 +446,63 @@ int launch_direct(const void* in, void* out, const void* hist, long long nframes
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
-// width: 16 (vload4), 8 (vload2) or 0 (element loads)
+template <typename T, typename A, int C, int F>
+int launch_direct_block(const Sig& sg, int k, int block, hipStream_t st) {
+  switch (block == 0 ? kWG : block_wg(block)) {
+    case 64: return launch_direct<T, A, C, F, 1, 64>(sg, k, st);
+    case 128: return launch_direct<T, A, C, F, 1, 128>(sg, k, st);
+    case 512: return launch_direct<T, A, C, F, 1, 512>(sg, k, st);
+    case 1024: return launch_direct<T, A, C, F, 1, 1024>(sg, k, st);
+    default: return launch_direct<T, A, C, F, 1, kWG>(sg, k, st);
+  }
+}
+
+// width: 16 (vload4), 8 (vload2) or 0 (one frame per lane); block: the
+// reference's block size (0 = 256 threads)
 template <typename T, typename A, int C>
-int dispatch_direct_c(int width, const void* in, void* out, const void* hist, long long nframes, int k,
-                      hipStream_t st) {
+int dispatch_direct_c(int width, const Sig& sg, int k, int block, hipStream_t st) {
   constexpr int FB = C * (int)sizeof(T);
   constexpr int F16 = (FB <= 16 && 16 % FB == 0) ? 16 / FB : 0;
   constexpr int F8 = (FB <= 8 && 8 % FB == 0) ? 8 / FB : 0;
   if constexpr (F16 > 0) {
-    if (width == 16) return launch_direct<T, A, C, F16>(in, out, hist, nframes, k, st);
+    if (width == 16) return launch_direct_block<T, A, C, F16>(sg, k, block, st);
   }
   if constexpr (F8 > 0) {
-    if (width >= 8) return launch_direct<T, A, C, F8>(in, out, hist, nframes, k, st);
+    if (width >= 8) return launch_direct_block<T, A, C, F8>(sg, k, block, st);
   }
-  return launch_direct<T, A, C, 1>(in, out, hist, nframes, k, st);
+  return launch_direct_block<T, A, C, 1>(sg, k, block, st);
 }
 
 template <typename T, typename A>
-int dispatch_direct(int C, int width, const void* in, void* out, const void* hist, long long nframes, int k,
-                    hipStream_t st) {
+int dispatch_direct(int C, int width, const Sig& sg, int k, int block, hipStream_t st) {
   switch (C) {
-    case 1: return dispatch_direct_c<T, A, 1>(width, in, out, hist, nframes, k, st);
-    case 2: return dispatch_direct_c<T, A, 2>(width, in, out, hist, nframes, k, st);
-    case 3: return dispatch_direct_c<T, A, 3>(width, in, out, hist, nframes, k, st);
-    case 4: return dispatch_direct_c<T, A, 4>(width, in, out, hist, nframes, k, st);
-    case 5: return dispatch_direct_c<T, A, 5>(width, in, out, hist, nframes, k, st);
-    case 6: return dispatch_direct_c<T, A, 6>(width, in, out, hist, nframes, k, st);
-    case 7: return dispatch_direct_c<T, A, 7>(width, in, out, hist, nframes, k, st);
-    case 8: return dispatch_direct_c<T, A, 8>(width, in, out, hist, nframes, k, st);
+    case 1: return dispatch_direct_c<T, A, 1>(width, sg, k, block, st);
+    case 2: return dispatch_direct_c<T, A, 2>(width, sg, k, block, st);
+    case 3: return dispatch_direct_c<T, A, 3>(width, sg, k, block, st);
+    case 4: return dispatch_direct_c<T, A, 4>(width, sg, k, block, st);
+    case 5: return dispatch_direct_c<T, A, 5>(width, sg, k, block, st);
+    case 6: return dispatch_direct_c<T, A, 6>(width, sg, k, block, st);
+    case 7: return dispatch_direct_c<T, A, 7>(width, sg, k, block, st);
+    case 8: return dispatch_direct_c<T, A, 8>(width, sg, k, block, st);
     default: return MAVG_ERR_UNSUPPORTED;
   }
 }
 
+// naive: one thread per sample, exactly `block` threads per workgroup (any
+// multiple of 32 in [32, 1024], as the reference launches; 0 = 256)
 template <typename T, typename A>
-int launch_naive(const void* in, void* out, const void* hist, long long nframes, int C, int k, hipStream_t st) {
-  const long long n = nframes * C;
-  const long long nblk = (n + kWG - 1) / kWG;
+int launch_naive(const Sig& sg, int C, int k, int block, hipStream_t st) {
+  const int wg = block == 0 ? kWG : block;
+  const long long n = sg.nframes * C;
+  const long long nblk = (n + wg - 1) / wg;
   if (nblk > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text), "naive<%s,acc=%s> grid=%lld block=%d", type_name<T>(),
-             type_name<A>(), nblk, kWG);
+             type_name<A>(), nblk, wg);
     return MAVG_OK;
   }
-  hipLaunchKernelGGL((naive_kernel<T, A>), dim3((unsigned)nblk), dim3(kWG), 0, st, static_cast<const T*>(in),
-                     static_cast<T*>(out), static_cast<const T*>(hist), nframes, C, k, make_out_params(k));
+  hipLaunchKernelGGL((naive_kernel<T, A>), dim3((unsigned)nblk), dim3(wg), 0, st, static_cast<const T*>(sg.in),
+                     static_cast<T*>(sg.out), static_cast<const T*>(sg.hist), sg.nframes, C, k, make_out_params(k));
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 

@@ -19,7 +19,7 @@ template <> struct ScanAcc<int16_t, int64_t> { using type = int32_t; };
 template <typename T, int C, int F, int U, int WG, int NT>
 __device__ __forceinline__ void stage_shifted_load(const T* __restrict__ in, const T* __restrict__ hist,
                                                    Unit<T, F * C> (&h)[U + 1], long long h0, long long nframes,
-                                                   int k, int tid) {
+                                                   int k, int pre, bool eio, int tid) {
   constexpr int VE = F * C;
   using IO = UnitIO<T, VE>;
   using U_t = Unit<T, VE>;
@@ -30,14 +30,14 @@ __device__ __forceinline__ void stage_shifted_load(const T* __restrict__ in, con
 #pragma unroll
     for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-      for (int c = 0; c < C; ++c) r.e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+      for (int c = 0; c < C; ++c) r.e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k, pre);
     return r;
   };
   if (fast) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      h[u] = IO::template load<(NT & kNtHalo) != 0>(in + (h0 + (long long)(u * WG + tid) * F) * C);
-    if (tid == 0) h[U] = IO::template load<(NT & kNtHalo) != 0>(in + (h0 + (long long)(U * WG) * F) * C);
+      h[u] = IO::template gload<(NT & kNtHalo) != 0>(in + (h0 + (long long)(u * WG + tid) * F) * C, eio);
+    if (tid == 0) h[U] = IO::template gload<(NT & kNtHalo) != 0>(in + (h0 + (long long)(U * WG) * F) * C, eio);
   } else {
 #pragma unroll
     for (int u = 0; u < U; ++u) h[u] = guarded(u * WG + tid);
@@ -55,9 +55,10 @@ __device__ __forceinline__ void stage_shifted_store(T* stage, const Unit<T, F * 
 // Both halves in one call (ORD 0/1).
 template <typename T, int C, int F, int U, int WG, int NT>
 __device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, const T* __restrict__ hist,
-                                                   T* stage, long long h0, long long nframes, int k, int tid) {
+                                                   T* stage, long long h0, long long nframes, int k, int pre,
+                                                   bool eio, int tid) {
   Unit<T, F * C> h[U + 1];
-  stage_shifted_load<T, C, F, U, WG, NT>(in, hist, h, h0, nframes, k, tid);
+  stage_shifted_load<T, C, F, U, WG, NT>(in, hist, h, h0, nframes, k, pre, eio, tid);
   stage_shifted_store<T, C, F, U, WG>(stage, h, tid);
 }
 
@@ -174,6 +175,8 @@ struct AheadParams {
   int ahead;        // D (a multiple of 8): block b publishes the records of block b + D's tile
   int head;         // whole tiles a window can span (k / T): the head duty of remap mode 1
   int spin;         // polls of an untagged granule before recomputing it
+  int pre;          // frames in front of `in` that are readable signal (load_elem)
+  int eio;          // frame-unit launch on element-aligned pointers (UnitIO::gload)
   unsigned long long* gran;  // [nfull][C][NG] granules, zeroed before the launch
   void* stats;               // MAVG_AHEAD_STATS builds only: {recomputes, polls that waited}
   OutParams o;
@@ -214,6 +217,8 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   const int w = tid >> 6;
   const int k = p.k;
   const long long nframes = p.nframes;
+  const int pre = p.pre;
+  const bool eio = F == 1 && p.eio != 0;
 
   const long long tile = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
   const long long t0 = tile * TF;
@@ -235,7 +240,7 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   auto load_a = [&]() {
     if (produce)
 #pragma unroll
-      for (int u = 0; u < U; ++u) xa[u] = IO::load(in + (ja * TF + (long long)(u * WG + tid) * F) * C);
+      for (int u = 0; u < U; ++u) xa[u] = IO::gload(in + (ja * TF + (long long)(u * WG + tid) * F) * C, eio);
   };
   // source 0 = phase A (tile ja), 1 = own tile, 2 = head duty: each wave
   // leaves its share in LDS, published after the first barrier
@@ -257,12 +262,12 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
     for (int u = 0; u < U; ++u) {
       const long long f = t0 + (long long)(u * WG + tid) * F;
       if (tile_full) {
-        x[u] = IO::template load<(NT & kNtLoad) != 0>(in + f * C);
+        x[u] = IO::template gload<(NT & kNtLoad) != 0>(in + f * C, eio);
       } else {
 #pragma unroll
         for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-          for (int c = 0; c < C; ++c) x[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+          for (int c = 0; c < C; ++c) x[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k, pre);
       }
     }
   };
@@ -270,16 +275,16 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
     load_a();
     publish_a();
     load_tile();
-    stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, tid);
+    stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, pre, eio, tid);
   } else if constexpr (ORD == 1) {
     load_a();
     load_tile();
     publish_a();
-    stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, tid);
+    stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, pre, eio, tid);
   } else {
     U_t hs[U + 1];
     load_tile();
-    stage_shifted_load<T, C, F, U, WG, NT>(in, hist, hs, h0, nframes, k, tid);
+    stage_shifted_load<T, C, F, U, WG, NT>(in, hist, hs, h0, nframes, k, pre, eio, tid);
     load_a();
     stage_shifted_store<T, C, F, U, WG>(stage, hs, tid);
     publish_a();
@@ -304,7 +309,7 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   if (jh >= 0) {
     U_t xh[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) xh[u] = IO::load(in + (jh * TF + (long long)(u * WG + tid) * F) * C);
+    for (int u = 0; u < U; ++u) xh[u] = IO::gload(in + (jh * TF + (long long)(u * WG + tid) * F) * C, eio);
     SA r[C];
     wave_record<T, SA, C, F, U>(xh, r);
     share(2, r);
@@ -346,10 +351,10 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
     for (int i = tid; i < pcount; i += WG)
 #pragma unroll
       for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(stage[(s0 + i) * C + c]);
-  } else if (hist != nullptr) {
+  } else if (hist != nullptr || pre > 0) {  // frames before 0: history and/or the peeled head
     for (long long f = a + tid; f < 0; f += WG)
 #pragma unroll
-      for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(load_elem(in, hist, f, c, C, nframes, k));
+      for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(load_elem(in, hist, f, c, C, nframes, k, pre));
   }
 
   // ---- d = x - x[n-k]; in-lane, wave and segment scans ----
@@ -463,7 +468,8 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
       for (int wv = 0; wv < NW; ++wv) {  // its NW wave shares, in wave order
         U_t xr[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) xr[u] = IO::load(in + (jj * TF + (long long)(u * WG + wv * 64 + lane) * F) * C);
+        for (int u = 0; u < U; ++u)
+          xr[u] = IO::gload(in + (jj * TF + (long long)(u * WG + wv * 64 + lane) * F) * C, eio);
         SA rw[C];
         wave_record<T, SA, C, F, U>(xr, rw);
 #pragma unroll
@@ -532,7 +538,7 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
           y.e[fr * C + c] = to_out<T, A>(base[u][c] + (A)(lx[u][c] + v[u][fr][c]), p.o);
     }
     if (tile_full) {
-      IO::template store<(NT & kNtStore) != 0>(out + f * C, y);
+      IO::template gstore<(NT & kNtStore) != 0>(out + f * C, y, eio);
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)

@@ -11,16 +11,16 @@ namespace mavg {
 // of reading before the buffer).
 // ----------------------------------------------------------------------------
 template <typename T, typename A>
-__global__ __launch_bounds__(kWG) void naive_kernel(const T* __restrict__ in, T* __restrict__ out,
-                                                    const T* __restrict__ hist, long long nframes,
-                                                    int C, int k, OutParams o) {
-  const long long idx = (long long)blockIdx.x * kWG + threadIdx.x;
+__global__ __launch_bounds__(1024) void naive_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                     const T* __restrict__ hist, long long nframes,
+                                                     int C, int k, OutParams o) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long n = nframes * C;
   if (idx >= n) return;
   const long long f = idx / C;
   const int c = (int)(idx - f * C);
   A s = (A)0;
-  for (int j = 0; j < k; ++j) s += to_acc<A>(load_elem(in, hist, f - j, c, C, nframes, k));
+  for (int j = 0; j < k; ++j) s += to_acc<A>(load_elem(in, hist, f - j, c, C, nframes, k, 0));
   out[idx] = to_out<T, A>(s, o);
 }
 

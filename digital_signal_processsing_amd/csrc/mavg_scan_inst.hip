@@ -5,6 +5,5 @@
 #include "mavg_launch.hpp"
 
 namespace mavg {
-template int dispatch_scan_c<MAVG_T, MAVG_A, MAVG_C>(bool, bool, const void*, void*, const void*, long long, int,
-                                                     hipStream_t, Workspace);
+template int dispatch_scan_c<MAVG_T, MAVG_A, MAVG_C>(bool, bool, const Sig&, int, int, hipStream_t, Workspace);
 }  // namespace mavg

@@ -21,6 +21,8 @@ struct ScanParams {
   int xk_off;            // (-k*C) mod VE, elements: offset of x[n-k] inside its aligned unit
   int xkg;               // 1: read x[n-k] from global memory (k too large for the LDS ring)
   int xcd_remap;         // remap mode (remap_tile): 0 identity, 1 contiguous per XCD, G>1 grouped
+  int pre;               // frames in front of `in` that are readable signal (load_elem)
+  int eio;               // frame-unit launch on element-aligned pointers (UnitIO::gload)
   OutParams o;
 };
 
@@ -55,6 +57,8 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
   const long long nframes = p.nframes;
   const int k = p.k;
   const int R = p.ring_frames;
+  const int pre = p.pre;
+  const bool eio = F == 1 && p.eio != 0;
 
   const long long seg = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
   const long long s0 = seg * p.seg_frames;
@@ -68,7 +72,7 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long long f = c0 + (long long)(u * kWG + tid) * F;
-        buf[u] = IO::template load<(NT & kNtLoad) != 0>(in + f * C);
+        buf[u] = IO::template gload<(NT & kNtLoad) != 0>(in + f * C, eio);
       }
     } else {
 #pragma unroll
@@ -78,7 +82,7 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
         for (int fr = 0; fr < F; ++fr)
 #pragma unroll
           for (int c = 0; c < C; ++c)
-            buf[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+            buf[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k, pre);
       }
     }
   };
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
         for (int fr = 0; fr < F; ++fr)
 #pragma unroll
           for (int c = 0; c < C; ++c)
-            xk.e[fr * C + c] = (f + fr < p0) ? (T)0 : load_elem(in, hist, f + fr, c, C, nframes, k);
+            xk.e[fr * C + c] = (f + fr < p0) ? (T)0 : load_elem(in, hist, f + fr, c, C, nframes, k, pre);
       } else if constexpr (IO::kVec) {
         int qk = kb + j * F;
         if (qk >= R) qk -= R;
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
           for (int c = 0; c < C; ++c)
             y.e[fr * C + c] = to_out<T, A>(base[u][c] + lx[u][c] + v[u][fr][c], p.o);
         if (full) {
-          IO::template store<(NT & kNtStore) != 0>(out + f * C, y);
+          IO::template gstore<(NT & kNtStore) != 0>(out + f * C, y, eio);
         } else {
 #pragma unroll
           for (int fr = 0; fr < F; ++fr)

@@ -31,6 +31,8 @@ struct TileParams {
   int halo_units;  // ceil(k / F): units staged before the tile
   int xk_off;      // (-k*C) mod VE
   int xcd_remap;   // remap mode (remap_tile): 0 identity, 1 contiguous per XCD, G>1 grouped
+  int pre;         // frames in front of `in` that are readable signal (load_elem)
+  int eio;         // frame-unit launch on element-aligned pointers (UnitIO::gload)
   OutParams o;
 };
 
@@ -72,6 +74,8 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   const int w = tid >> 6;
   const int k = p.k;
   const long long nframes = p.nframes;
+  const int pre = p.pre;
+  const bool eio = F == 1 && p.eio != 0;
 
   // bijective XCD-aware remap (cdna_hip_programming.md 5.5 T1): blocks b and
   // b+8 share an XCD; give each XCD a contiguous run of tiles.
@@ -88,16 +92,16 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
     if (tile_full) {
       if constexpr ((NT & kNtSplit) != 0) {
         // frames the next tile's halo re-reads keep the default policy (L2)
-        if ((u * WG + tid) * F + F > TF - Ha) x[u] = IO::template load<false>(in + f * C);
-        else x[u] = IO::template load<true>(in + f * C);
+        if ((u * WG + tid) * F + F > TF - Ha) x[u] = IO::template gload<false>(in + f * C, eio);
+        else x[u] = IO::template gload<true>(in + f * C, eio);
       } else {
-        x[u] = IO::template load<(NT & kNtLoad) != 0>(in + f * C);
+        x[u] = IO::template gload<(NT & kNtLoad) != 0>(in + f * C, eio);
       }
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-        for (int c = 0; c < C; ++c) x[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+        for (int c = 0; c < C; ++c) x[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k, pre);
     }
   }
   // ---- halo -> LDS (re-read of the previous tile's tail: L2) ----
@@ -107,12 +111,12 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
       const long long f = h0 + (long long)j * F;
       U_t h;
       if (halo_fast) {
-        h = IO::template load<(NT & kNtHalo) != 0>(in + f * C);
+        h = IO::template gload<(NT & kNtHalo) != 0>(in + f * C, eio);
       } else {
 #pragma unroll
         for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-          for (int c = 0; c < C; ++c) h.e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k);
+          for (int c = 0; c < C; ++c) h.e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k, pre);
       }
       IO::store(stage + j * VE, h);
     }
@@ -277,7 +281,7 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
         for (int c = 0; c < C; ++c) y.e[fr * C + c] = to_out<T, A>(base[u][c] + lx[u][c] + v[u][fr][c], p.o);
     }
     if (tile_full) {
-      IO::template store<(NT & kNtStore) != 0>(out + f * C, y);
+      IO::template gstore<(NT & kNtStore) != 0>(out + f * C, y, eio);
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)

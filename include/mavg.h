@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define MAVG_ABI_VERSION 1
+#define MAVG_ABI_VERSION 2  /* 2: mavg_plan takes block_size; mavg_test_ahead_schedule */
 
 typedef enum {
     MAVG_I16 = 0, /* int16 PCM in/out (the reference's WAV data path) */
@@ -71,16 +71,18 @@ typedef enum {
     MAVG_OK = 0,
     MAVG_ERR_INVALID_ARG = 1, /* null pointer, k < 1, C < 1, n not a multiple of C, bad enum */
     MAVG_ERR_UNSUPPORTED = 2, /* valid but not implemented (C > 8 outside AUTO/NAIVE, k too large for algo) */
-    MAVG_ERR_MISALIGNED = 3,  /* a 16-B-unit algorithm got a pointer not 16-B aligned */
+    MAVG_ERR_MISALIGNED = 3,  /* a pointer not aligned to the sample size (2 B int16, 4 B fp32) */
     MAVG_ERR_WORKSPACE = 4,   /* ws_bytes smaller than mavg_workspace_bytes() */
     MAVG_ERR_HIP = 5          /* a HIP runtime call or kernel launch failed */
 } mavg_status;
 
-/* Device workspace (bytes) mavg_run needs for this problem.  0 for every
- * launch except the look-ahead scan that AUTO/BLELLOCH pick for windows too
- * long for an LDS-staged halo (fp32 halos > 16 KiB, e.g. mono k > 4096;
- * int16 past ~47 KiB): 8 B per (whole tile, channel, 32-bit word of the
- * tile sum), padded to 16, + 16 (4 MiB for 2^30 fp32 samples).
+/* Device workspace (bytes) mavg_run needs for this problem, whatever the
+ * alignment of the views later passed to mavg_run.  0 for every launch
+ * except the look-ahead scan that AUTO/BLELLOCH pick for windows too long
+ * for an LDS-staged halo (fp32 halos > 16 KiB, e.g. mono k > 4096; int16 past
+ * ~47 KiB): 8 B per (whole tile, channel, 32-bit word of the tile sum),
+ * padded to 16, + 16, for the smaller tiles of the frame-unit form (16 MiB for
+ * 2^30 fp32 mono samples; a misaligned view may run that form).
  * 16-B alignment; contents need no initialisation (mavg_run zeroes them on
  * the stream); one workspace must not serve two launches that may run
  * concurrently. */
@@ -89,12 +91,19 @@ int mavg_workspace_bytes(size_t n_samples, int channels, int grade, int dtype,
 
 /*
  * y[0..n) = moving average of x[0..n), n = frames * channels samples.
+ *   d_in/d_out any sample-aligned views (2 B int16, 4 B fp32): a vector
+ *              algorithm on views that are not 16-B aligned peels a head of
+ *              < 16 B in its one-frame-per-lane form when both views share
+ *              the offset, else runs that form over the whole signal.
  *   d_history  NULL (zero history) or (grade-1)*channels samples that
- *              precede d_in (any alignment).
- *   block_size the reference's argv block size (multiple of 32 in
- *              [32, 1024]) or 0; accepted for drop-in compatibility (the
- *              CLIs log it), while every MI355X kernel uses its tuned
- *              256-thread (4 x wave64) workgroup.
+ *              precede d_in (sample-aligned).
+ *   block_size the reference's argv block size (a multiple of 32 in
+ *              [32, 1024]) or 0 for the tuned geometry.  Non-zero: the naive
+ *              kernel runs exactly block_size threads per workgroup; the tile
+ *              scans and the direct kernel run the next power of two of at
+ *              least one wave64 (64, 128, 256, 512, 1024), while the window's
+ *              halo fits that workgroup's LDS (longer windows keep the tuned
+ *              look-ahead / segment scan).  mavg_plan() shows the result.
  *   stream     hipStream_t or NULL.
  * Returns a mavg_status.  Nothing is enqueued unless MAVG_OK is returned
  * (MAVG_ERR_HIP excepted, when the launch itself failed).
@@ -104,9 +113,10 @@ int mavg_run(const void* d_in, void* d_out, size_t n_samples, int channels,
              const void* d_history, void* d_ws, size_t ws_bytes, void* stream);
 
 /* Describe, without launching anything, the kernel and launch geometry
- * mavg_run would use for these arguments (e.g. "tile_scan<f32,...> grid=..."). */
+ * mavg_run would use for these arguments on 16-B-aligned views
+ * (e.g. "tile_scan<f32,...> grid=... block=256 ..."). */
 int mavg_plan(size_t n_samples, int channels, int grade, int dtype, int algo,
-              char* buf, size_t buflen);
+              int block_size, char* buf, size_t buflen);
 
 /* The algorithm MAVG_ALGO_AUTO resolves to for these arguments. */
 int mavg_resolve_algo(size_t n_samples, int channels, int grade, int dtype, int algo);
@@ -123,6 +133,14 @@ int mavg_fill_synthetic(void* d_out, size_t n_samples, int dtype, uint64_t seed,
  * read against the same box's achievable streaming rate.  bytes a multiple
  * of 16, both pointers 16-B aligned. */
 int mavg_stream_copy(const void* d_in, void* d_out, size_t bytes, void* stream);
+
+/* TEST HOOK (parity tests only): override the look-ahead scan's schedule --
+ * `slots` dispatch slots between a record's producer and its consumers
+ * (default 512), `spin` polls of an unpublished record before the consumer
+ * recomputes it (default 256); a negative value restores the default.
+ * Outputs are bitwise identical for every setting; only the path that
+ * produces a record changes.  Process-wide; returns MAVG_OK. */
+int mavg_test_ahead_schedule(int slots, int spin);
 
 const char* mavg_strerror(int status);
 const char* mavg_algo_name(int algo);

@@ -24,7 +24,7 @@ def test_library_exports_every_symbol():
     lib = _lib.load()
     for name in _header_symbols():
         assert hasattr(lib, name), name
-    assert lib.mavg_abi_version() == 1
+    assert lib.mavg_abi_version() == 2
 
 
 def test_strerror_and_names():
@@ -34,9 +34,9 @@ def test_strerror_and_names():
         assert _lib.algo_name(code) == name
 
 
-def _run(n, C, k, dtype=_lib.F32, algo=0, din=16, dout=16, hist=None):
+def _run(n, C, k, dtype=_lib.F32, algo=0, din=16, dout=16, hist=None, block=0):
     lib = _lib.load()
-    return lib.mavg_run(din, dout, n, C, k, dtype, algo, 0, hist, None, 0, None)
+    return lib.mavg_run(din, dout, n, C, k, dtype, algo, block, hist, None, 0, None)
 
 
 @pytest.mark.parametrize("args,status", [
@@ -48,7 +48,13 @@ def _run(n, C, k, dtype=_lib.F32, algo=0, din=16, dout=16, hist=None):
     (dict(n=10, C=1, k=3, dtype=7), _lib.ERR_INVALID_ARG),
     (dict(n=10, C=1, k=3, algo=99), _lib.ERR_INVALID_ARG),
     (dict(n=10, C=1, k=3, din=0), _lib.ERR_INVALID_ARG),  # null input
-    (dict(n=8, C=1, k=3, din=20), _lib.ERR_MISALIGNED),   # vector algo, unaligned
+    (dict(n=8, C=1, k=3, din=18), _lib.ERR_MISALIGNED),   # fp32 view not 4-B aligned
+    (dict(n=8, C=1, k=3, dout=22), _lib.ERR_MISALIGNED),
+    (dict(n=8, C=1, k=3, dtype=_lib.I16, din=21), _lib.ERR_MISALIGNED),  # int16 view not 2-B aligned
+    (dict(n=8, C=1, k=3, hist=19), _lib.ERR_MISALIGNED),  # history not sample-aligned
+    (dict(n=8, C=1, k=3, block=48), _lib.ERR_INVALID_ARG),    # reference: a multiple of 32 in [32, 1024]
+    (dict(n=8, C=1, k=3, block=2048), _lib.ERR_INVALID_ARG),
+    (dict(n=8, C=1, k=3, block=16), _lib.ERR_INVALID_ARG),
     (dict(n=0, C=1, k=3, din=0, dout=0), _lib.OK),        # empty input is a no-op
 ])
 def test_run_validates_before_launch(args, status):
@@ -119,16 +125,20 @@ def test_workspace_only_for_ahead_scan():
     # type), padded to 16 bytes, plus 16 bytes of statistics
     assert dsp.workspace_bytes(1 << 30, 1024) == 0
     assert dsp.workspace_bytes(1 << 30, 4096) == 0
-    # fp32 halos past 16 KiB take the look-ahead scan (U=4: 4096-frame tiles)
+    # fp32 halos past 16 KiB take the look-ahead scan (U=4: 4096-frame tiles);
+    # the workspace is sized for the frame-unit form too (1024-frame tiles),
+    # which a view that is not 16-B aligned may run
     tiles = (1 << 30) // 4096
     assert dsp.plan(1 << 30, 8192).startswith("ahead_scan<f32,acc=f64,C=1,F=4,U=4")
-    assert dsp.workspace_bytes(1 << 30, 8192) == tiles * 2 * 8 + 16
     assert "ws=%d" % (tiles * 2 * 8 + 16) in dsp.plan(1 << 30, 20_000)
+    assert dsp.plan(1 << 30, 8192, algo="blelloch_scalar").startswith("ahead_scan<f32,acc=f64,C=1,F=1,U=4")
+    assert dsp.workspace_bytes(1 << 30, 8192) == 4 * tiles * 2 * 8 + 16
+    assert dsp.workspace_bytes(1 << 30, 8192, algo="blelloch_scalar") == 4 * tiles * 2 * 8 + 16
     assert dsp.plan(1 << 30, 8192, algo="hillis").startswith("segment_scan<")
     # int16 keeps the 1024-thread tile up to ~47 KiB of halo
     assert dsp.workspace_bytes(1 << 30, 8192, dtype=dsp.I16) == 0
     n = 2 * 1_000_003
-    st = (n // 2) // 4096     # int16 stereo: one int32 word per (whole tile, channel)
+    st = (n // 2) // 1024     # int16 stereo, frame-unit tiles: one int32 word per (whole tile, channel)
     assert dsp.workspace_bytes(n, 44100, 2, dsp.I16) == (st * 2 * 8 + 15) // 16 * 16 + 16
     assert dsp.workspace_bytes(1 << 20, 70_000, algo="hillis") == 0
     assert dsp.workspace_bytes(0, 70_000) == 0
@@ -153,3 +163,31 @@ def test_many_channels_auto_resolves_to_naive():
     import digital_signal_processsing_amd as dsp
     assert dsp.resolve_algo(16 * 100, 5, channels=16) == "naive"
     assert dsp.plan(16 * 100, 5, channels=16).startswith("naive<")
+
+
+@pytest.mark.parametrize("algo,block,want", [
+    ("blelloch", 512, "block=512"), ("blelloch", 256, "block=256"), ("blelloch", 1024, "block=1024"),
+    ("blelloch", 32, "block=64"), ("blelloch", 96, "block=128"), ("blelloch", 128, "block=128"),
+    ("hillis", 64, "block=64"), ("blelloch_scalar", 512, "block=512"), ("hillis_scalar", 1024, "block=1024"),
+    ("direct", 128, "block=128"), ("direct_vec2", 1024, "block=1024"), ("direct_scalar", 64, "block=64"),
+    ("naive", 96, "block=96"), ("naive", 32, "block=32"), ("naive", 0, "block=256"),
+])
+def test_block_size_sets_the_workgroup(algo, block, want):
+    """The reference launches its kernels with the argv block size
+    (blelloch_scan_averager.cu:155,215-217); here the naive kernel runs it
+    exactly and the tiled kernels run the next power of two >= one wave64."""
+    import digital_signal_processsing_amd as dsp
+    p = dsp.plan(1 << 20, 64, algo=algo, block_size=block)
+    assert re.search(r"block=\d+", p).group(0) == want, p
+
+
+def test_block_size_tuned_and_fallback_geometry():
+    import digital_signal_processsing_amd as dsp
+    assert dsp.plan(1 << 20, 1024, block_size=0) == dsp.plan(1 << 20, 1024)
+    # U=2 tiles at the requested workgroup: 64 threads x 4 frames x 2
+    assert "tile_frames=512" in dsp.plan(1 << 20, 64, algo="blelloch", block_size=64)
+    # a window whose halo does not fit the requested workgroup's LDS keeps the tuned launch
+    assert dsp.plan(1 << 20, 70_000, block_size=512) == dsp.plan(1 << 20, 70_000)
+    assert dsp.plan(1 << 20, 70_000, block_size=512).startswith("ahead_scan<")
+    with pytest.raises(dsp.MavgError):
+        dsp.plan(1 << 20, 64, block_size=48)

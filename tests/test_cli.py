@@ -249,3 +249,24 @@ def test_harness_baseline_configs_verify():
     for c in (1, 2, 3, 4, 5):
         assert f"\n#{c} " in r.stdout
     assert r.stdout.count("0 mismatches") >= 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,block,want", [("bin_vblelloch", 512, 512), ("bin_vblelloch", 32, 64),
+                                             ("bin_blelloch", 1024, 1024), ("bin_vhillis", 128, 128),
+                                             ("bin_vec4", 1024, 1024), ("bin_shared", 64, 64),
+                                             ("bin_parallel", 96, 96), ("bin_parallel", 1024, 1024)])
+def test_gpu_bins_run_the_argv_block_size(tmp_path, stereo_wav, oracle_mod, name, block, want):
+    """The reference launches with the argv block size (blelloch_scan_averager.cu:
+    155,215-217; run_benchmarks.py:21 sweeps 32..1024): the launch each binary
+    reports runs that workgroup (naive exactly, tiled kernels the next power of
+    two >= one wave64), and the output is unchanged."""
+    import re
+    path, data = stereo_wav
+    r = _run(name, path, 41, block, "--out", tmp_path / "o.wav", cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    kern = [l for l in r.stdout.splitlines() if l.startswith("Kernel: ")]
+    assert kern and re.search(r"block=(\d+)", kern[0]).group(1) == str(want), kern
+    assert np.array_equal(rb.read_wav_samples(str(tmp_path / "o.wav")), oracle_mod.mavg_i16(data.reshape(-1), 41, 2))
+    rows = list(csv.reader(open(tmp_path / "benchmark_data.csv")))
+    assert rows[1][4] == str(block)

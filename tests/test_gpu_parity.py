@@ -187,11 +187,9 @@ def test_sharded_split_launch_equals_whole_signal(oracle_mod, gpu, C, k, dtype):
     for r in range(world):
         f0, f1 = shard_bounds(frames, world, r)
         hist = xd[(f0 - (k - 1)) * C: f0 * C] if (r > 0 and k > 1) else None
-        # shards must start 16-B aligned for the vector kernels: copy each into its own buffer
-        xl = xd[f0 * C: f1 * C].clone()
-        ol = torch.empty_like(xl)
-        split_moving_average_into(xl, ol, k, C, "blelloch", history=hist.clone() if hist is not None else None)
-        out[f0 * C: f1 * C] = ol
+        # views straight into the whole signal: shards cut at any frame, so
+        # neither the shard nor its history is 16-B aligned in general
+        split_moving_average_into(xd[f0 * C: f1 * C], out[f0 * C: f1 * C], k, C, "blelloch", history=hist)
     y = out.cpu().numpy()
     if dtype == "i16":
         assert np.array_equal(y, full)
@@ -393,18 +391,15 @@ def test_ahead_large_stereo_slices(oracle_mod, gpu):
         assert np.array_equal(y[s * C:(s + span) * C], ref), f"slice at frame {s}"
 
 
-def _with_env(env, fn):
-    import os
-    old = {k: os.environ.get(k) for k in env}
+def _with_schedule(sched, fn):
+    """Run fn under a forced look-ahead schedule (mavg_test_ahead_schedule)."""
+    from digital_signal_processsing_amd import _lib
+    lib = _lib.load()
+    lib.mavg_test_ahead_schedule(sched.get("slots", -1), sched.get("spin", -1))
     try:
-        os.environ.update({k: str(v) for k, v in env.items()})
         return fn()
     finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        lib.mavg_test_ahead_schedule(-1, -1)
 
 
 @pytest.mark.parametrize("dtype,C,k", [("f32", 1, 20_000), ("f32", 3, 9_000), ("i16", 2, 44_100),
@@ -431,10 +426,9 @@ def test_ahead_records_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, 
     else:
         x = oracle_mod.synth_i16(frames * C, seed=77)
     base = _run(x, k, C, "auto", gpu)
-    for env in ({"MAVG_AHEAD_SPIN": 0}, {"MAVG_AHEAD_SLOTS": 0}, {"MAVG_AHEAD_SLOTS": 8},
-                {"MAVG_AHEAD_SLOTS": 1 << 28}, {"MAVG_AHEAD_SLOTS": 8, "MAVG_AHEAD_SPIN": 0}):
-        y = _with_env(env, lambda: _run(x, k, C, "auto", gpu))
-        assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), env
+    for sched in ({"spin": 0}, {"slots": 0}, {"slots": 8}, {"slots": 1 << 28}, {"slots": 8, "spin": 0}):
+        y = _with_schedule(sched, lambda: _run(x, k, C, "auto", gpu))
+        assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), sched
     if dtype == "f32":
         assert_f32_close(base, oracle_mod.mavg_f32(x, k, C), f"C={C} k={k}")
     else:
@@ -525,3 +519,104 @@ def test_dispatch_boundaries(oracle_mod, gpu, C, dtype):
         else:
             assert_f32_close(y, ref, f"k={k} frames={frames} hist={use_hist} {plan}")
     assert len(seen) >= 2, seen  # the sweep crosses kernel shapes (fp32 C=8: tile, look-ahead)
+
+
+MISALIGNED_CASES = [(dt, C, algo, k) for dt in ("f32", "i16") for C in (1, 2)
+                    for algo, k in (("blelloch", 37), ("blelloch", 1024), ("hillis", 300), ("direct", 9),
+                                    ("direct_vec2", 5), ("blelloch", 20_000))]
+
+
+@pytest.mark.parametrize("dt,C,algo,k", MISALIGNED_CASES)
+def test_misaligned_views(oracle_mod, gpu, dt, C, algo, k):
+    """Views that start 1..7 samples into an allocation: the same offset for
+    input and output (head peeled, vector body) and a fresh aligned output
+    (frame-unit form, element IO when a frame straddles its alignment).
+    Results equal the oracle's on the same samples: int16 bit-exact, fp32
+    within 1e-5 relative (the same bar as aligned launches)."""
+    import torch
+    import digital_signal_processsing_amd as dsp
+    frames = 40_003
+    base_n = frames * C + 16
+    xb = (oracle_mod.synth_i16(base_n, seed=31) if dt == "i16" else oracle_mod.synth_f32(base_n, seed=31, dist=1))
+    xd = torch.from_numpy(xb).to(gpu)
+    for off in range(1, 8):
+        n = (base_n - off) // C * C
+        xs = xb[off:off + n]
+        ref = oracle_mod.mavg_i16(xs, k, C) if dt == "i16" else oracle_mod.mavg_f32(xs, k, C)
+        # same offset for input and output
+        yb = torch.zeros_like(xd)
+        dsp.moving_average_into(xd[off:off + n], yb[off:off + n], k, C, algo)
+        # fresh (aligned) output
+        y2 = dsp.moving_average(xd[off:off + n], k, C, algo)
+        for y, what in ((yb[off:off + n], "same offset"), (y2, "fresh output")):
+            got = y.cpu().numpy()
+            if dt == "i16":
+                assert np.array_equal(got, ref), f"{what} off={off}"
+            else:
+                assert_f32_close(got, ref, f"{what} off={off}")
+        assert not yb[:off].any() and not yb[off + n:].any(), f"wrote outside the view, off={off}"
+
+
+@pytest.mark.parametrize("dt,C", [("f32", 1), ("i16", 2), ("f32", 2)])
+def test_misaligned_views_with_history(oracle_mod, gpu, dt, C):
+    """A misaligned shard whose history is a misaligned view too (what a shard
+    cut at an odd frame gets): equal to the whole-signal oracle."""
+    import torch
+    import digital_signal_processsing_amd as dsp
+    frames, k = 50_001, 777
+    x = oracle_mod.synth_i16(frames * C, seed=3) if dt == "i16" else oracle_mod.synth_f32(frames * C, seed=3, dist=1)
+    full = oracle_mod.mavg_i16(x, k, C) if dt == "i16" else oracle_mod.mavg_f32(x, k, C)
+    xd = torch.from_numpy(x).to(gpu)
+    out = torch.zeros_like(xd)
+    for f0 in (k - 1, 1001, 2047, 3333):
+        f1 = f0 + 9_999
+        dsp.moving_average_into(xd[f0 * C:f1 * C], out[f0 * C:f1 * C], k, C, "blelloch",
+                                history=xd[(f0 - k + 1) * C:f0 * C])
+        got = out[f0 * C:f1 * C].cpu().numpy()
+        if dt == "i16":
+            assert np.array_equal(got, full[f0 * C:f1 * C]), f0
+        else:
+            assert_f32_close(got, full[f0 * C:f1 * C], f"f0={f0}")
+
+
+BLOCK_ALGOS = ["blelloch", "blelloch_scalar", "hillis", "hillis_scalar", "direct", "direct_vec2", "direct_scalar",
+               "naive"]
+
+
+@pytest.mark.parametrize("dt,C", [("f32", 1), ("i16", 2), ("f32", 3)])
+def test_every_block_size_every_algo(oracle_mod, gpu, dt, C):
+    """Every reference block size (run_benchmarks.py:21, plus 96 and 160) on
+    every algorithm: the workgroup changes (mavg_plan), the output does not."""
+    import digital_signal_processsing_amd as dsp
+    frames = 30_011
+    x = oracle_mod.synth_i16(frames * C, seed=13) if dt == "i16" else oracle_mod.synth_f32(frames * C, seed=13, dist=1)
+    xd = _dev(x, gpu)
+    for k in (1, 7, 300, 3000):
+        ref = oracle_mod.mavg_i16(x, k, C) if dt == "i16" else oracle_mod.mavg_f32(x, k, C)
+        for algo in BLOCK_ALGOS:
+            if algo == "naive" and k == 3000:
+                continue
+            for block in (32, 64, 96, 128, 160, 256, 512, 1024):
+                got = dsp.moving_average(xd, k, C, algo, block_size=block).cpu().numpy()
+                if dt == "i16":
+                    assert np.array_equal(got, ref), (algo, block, k)
+                else:
+                    assert_f32_close(got, ref, f"{algo} block={block} k={k}")
+
+
+def test_explicit_side_stream_long_window(oracle_mod, gpu):
+    """stream= differing from the current stream, on the look-ahead scan (which
+    takes a workspace from the caching allocator): the workspace and the
+    output are allocated on the launch stream, which waits for the producer
+    of x on the current stream."""
+    import torch
+    import digital_signal_processsing_amd as dsp
+    n, k = 3_000_017, 50_000
+    s = torch.cuda.Stream()
+    for rep in range(3):
+        x = dsp.fill_synthetic(n, torch.float32, seed=40 + rep, dist=1, device=gpu)  # on the current stream
+        y = dsp.moving_average(x, k, stream=s)
+        del x  # freed on the current stream while s may still read it (record_stream keeps it alive)
+        s.synchronize()
+        assert_f32_close(y.cpu().numpy(), oracle_mod.mavg_f32(oracle_mod.synth_f32(n, seed=40 + rep, dist=1), k, 1),
+                         f"rep {rep}")

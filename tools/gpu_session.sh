@@ -27,7 +27,8 @@ for step in "$@"; do
   case $step in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     test) run pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=30 -p no:cacheprovider ;;
-    testx) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    testx) run pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread \
+            -p no:cacheprovider ;;
     bench) run bench 400 python bench.py --steps 20 --warmup 5 --all-workloads ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
             python bench.py --steps 10 --warmup 3 --no-cpu-baseline --all-workloads ;;
