@@ -49,6 +49,10 @@ WORKLOADS = {
     # a one-second window at 44.1 kHz: too long for an LDS-staged halo, so the
     # one-pass look-ahead scan (the inter-block carry path beyond config #4)
     "long_2p30": (1 << 30, 44100, 1, "f32", "blelloch"),
+    # the same one-second window on the reference's int16 PCM path (mono, and
+    # stereo as its WAV harness writes it)
+    "i16_long": (1 << 30, 44100, 1, "i16", "blelloch"),
+    "i16_stereo_long": (1 << 30, 44100, 2, "i16", "blelloch"),
 }
 
 

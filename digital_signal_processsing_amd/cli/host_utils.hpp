@@ -65,6 +65,14 @@ template <> struct MemoryTraits<MemoryMode::Standard> {
   }
 };
 
+// Managed memory (the reference's zero-copy mode, gpu_utils.h MemoryTraits):
+// the host writes the input in place and the kernel reads it where it lies.
+// Prefetching the pages to the GPU inside the H2D phase was measured
+// (profiles/r02_cli_unified_prefetch/): the kernel phase then drops from 2.59
+// to 0.042 ms on 50 M samples, but the migration takes 149 ms (H2D) + 30 ms
+// (D2H) on this driver (no XNACK), 19x the zero-copy form's 9.3 ms end to
+// end -- so the zero-copy form stays, and its Compute column includes the
+// link traffic by construction.
 template <> struct MemoryTraits<MemoryMode::Unified> {
   static const char* name() { return "Unified"; }
   static void allocate(void** p, size_t bytes) { HIP_CHECK(hipMallocManaged(p, bytes)); }

@@ -28,15 +28,12 @@ OutParams make_out_params(int k) {
   OutParams o{};
   o.k = k;
   o.inv_k = 1.0 / (double)k;
-  if (k >= 2) {
+  o.inv_up = o.inv_k * (1.0 + 0x1p-50);  // to_out_i16: the product stays above S/k by < 2^-48 relative
+  if (k >= 2 && k <= 65535) {  // to_out_i16_magic
     int l = 0;
-    while ((1LL << l) < (long long)k) ++l;                  // l = ceil(log2 k), 2^l >= k > 2^(l-1)
-    const uint64_t m = ((uint64_t)1 << (31 + l)) / (uint64_t)k + 1;  // < 2^32 for k <= 65535
-    o.magic = (uint32_t)m;
+    while ((1LL << l) < (long long)k) ++l;  // 2^l >= k > 2^(l-1)
+    o.magic = (uint32_t)(((uint64_t)1 << (31 + l)) / (uint64_t)k + 1);
     o.shift = l - 1;
-  } else {
-    o.magic = 0;
-    o.shift = 0;
   }
   return o;
 }

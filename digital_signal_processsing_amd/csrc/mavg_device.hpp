@@ -72,38 +72,55 @@ __device__ __forceinline__ int64_t shfl_up(int64_t v, int d) {
 // output conversion: window sum -> sample
 // ----------------------------------------------------------------------------
 struct OutParams {
-  double inv_k;     // 1/k (fp32 output, int64 path estimate)
-  uint32_t magic;   // int16/int32 path: q = umulhi(|S|, magic) >> shift
-  int shift;
+  double inv_k;     // 1/k (fp32 output)
+  double inv_up;    // (1/k)(1 + ~2^-50), rounded: the int16 quotient estimate (to_out_i16)
   int k;            // divisor
+  uint32_t magic;   // to_out_i16_magic: q = umulhi(|S|, magic) >> shift (k <= 65535)
+  int shift;
 };
 
 __device__ __forceinline__ float to_out_f32(double s, const OutParams& o) {
   return (float)(s * o.inv_k);
 }
-// exact C++ truncating division S / k for |S| < 2^31, k <= 65535
+// Exact C++ truncating division S / k for the int16 output: |S| <= 32768 k
+// (a sum of k int16 samples, so |S / k| <= 2^15) and k < 2^33.  With
+// inv_up = fl(fl(1/k) (1 + 2^-50)) the product P = fl(S inv_up) satisfies
+// S/k < P < (S/k)(1 + 2^-48) for S > 0 (every rounding factor lies within
+// 2^-52 of 1, the bias is 2^-50): an exact quotient q stays in [q, q + 2^-33)
+// and a non-integral one q + f (1/k <= f <= 1 - 1/k, 1/k > 2^-33) in
+// (q + f, q + f + 2^-33) -- truncation gives q either way; S < 0 mirrors it
+// (the product's sign is S's, v_cvt_i32_f64 truncates toward zero).  Three
+// full-rate VALU ops per sample (cvt, mul, cvt), no branches and no sign
+// fix-ups.  tests/test_division.py checks the rule against exact integer
+// division at every k <= 65535 and sampled k up to 2^31.
 __device__ __forceinline__ int16_t to_out_i16(int32_t s, const OutParams& o) {
-  uint32_t a = s < 0 ? (uint32_t)(-s) : (uint32_t)s;
-  uint32_t q = (o.k == 1) ? a : (__umulhi(a, o.magic) >> o.shift);
+  return (int16_t)(int32_t)((double)s * o.inv_up);
+}
+// The integer alternative for the int32 path: an unsigned magic-number
+// multiply on |S| (exact for |S| < 2^31, k <= 65535: the magic is
+// floor(2^(31+l) / k) + 1 with l = ceil(log2 k)), then the sign.
+__device__ __forceinline__ int16_t to_out_i16_magic(int32_t s, const OutParams& o) {
+  const uint32_t a = s < 0 ? (uint32_t)(-s) : (uint32_t)s;
+  const uint32_t q = o.k == 1 ? a : (__umulhi(a, o.magic) >> o.shift);
   return (int16_t)(s < 0 ? -(int32_t)q : (int32_t)q);
 }
-// exact truncating division for the int64 path (k > 65535; |S| <= 32768*k).
-// The quotient is at most 2^15, so the fp64 estimate fl(|S| * fl(1/k)) lies
-// within 2^15 * 2^-51.8 = 2^-36.8 of |S|/k, whose fractional part is 0 or at
-// least 1/k > 2^-31: truncation is exact except when k divides |S|, where it
-// may land one below -- fixed by one 32x32->64 multiply-compare, no loops.
+// int64 path (k > 65535): |S| <= 32768 k < 2^47 converts exactly from its
+// two halves, then the same product
 __device__ __forceinline__ int16_t to_out_i16(int64_t s, const OutParams& o) {
-  const uint64_t a = s < 0 ? (uint64_t)(-s) : (uint64_t)s;  // < 2^47
-  const double ad = (double)(uint32_t)(a >> 32) * 4294967296.0 + (double)(uint32_t)a;  // exact
-  uint32_t q = (uint32_t)(ad * o.inv_k);
-  q += a >= (uint64_t)(q + 1u) * (uint64_t)(uint32_t)o.k ? 1u : 0u;
-  return (int16_t)(s < 0 ? -(int32_t)q : (int32_t)q);
+  const double sd = (double)(int32_t)(s >> 32) * 4294967296.0 + (double)(uint32_t)s;  // exact
+  return (int16_t)(int32_t)(sd * o.inv_up);
 }
-template <typename T, typename A>
-__device__ __forceinline__ T to_out(A s, const OutParams& o);
-template <> __device__ __forceinline__ float to_out<float, double>(double s, const OutParams& o) { return to_out_f32(s, o); }
-template <> __device__ __forceinline__ int16_t to_out<int16_t, int32_t>(int32_t s, const OutParams& o) { return to_out_i16(s, o); }
-template <> __device__ __forceinline__ int16_t to_out<int16_t, int64_t>(int64_t s, const OutParams& o) { return to_out_i16(s, o); }
+// DV (int32 int16 path only): 0 = the fp64 product, 1 = the magic multiply
+template <typename T, typename A, int DV = 0>
+__device__ __forceinline__ T to_out(A s, const OutParams& o) {
+  if constexpr (sizeof(T) == 4) {
+    return to_out_f32(s, o);
+  } else if constexpr (DV == 1 && sizeof(A) == 4) {
+    return to_out_i16_magic(s, o);
+  } else {
+    return to_out_i16(s, o);
+  }
+}
 
 // ----------------------------------------------------------------------------
 // a "unit" = the F frames x C channels one lane owns per load instruction

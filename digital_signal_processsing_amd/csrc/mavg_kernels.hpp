@@ -27,9 +27,9 @@
 // Arithmetic: fp32 data accumulates in fp64 (a global fp32 prefix loses
 // 1e-4..1e-1 relative); int16 data accumulates exactly in
 // int32 (k <= 65535) or int64, and divides exactly (C++ truncation) with a
-// magic-number multiply (int32) or a corrected fp64 estimate (int64) -- NOT
-// the reference's float reciprocal, which is off on exact multiples
-// (SURVEY.md 0.4).
+// biased fp64 reciprocal product (to_out_i16, proof in its comment, checked by
+// tests/test_division.py) -- NOT the reference's float reciprocal, which is
+// off on exact multiples.
 #pragma once
 
 #include "mavg_device.hpp"

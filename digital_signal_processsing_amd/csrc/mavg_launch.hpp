@@ -142,8 +142,12 @@ int launch_scan(const Sig& sg, int k, hipStream_t st, ScanTuning tune = ScanTuni
 }
 
 // flat-tile scan: one workgroup per tile, carry rebuilt from the k-frame halo
+// DV: the int16 output division of the tile scan -- the magic multiply, which
+// measured faster than the fp64 product here (int16 stereo k=1024: 0.779 vs
+// 0.763 of peak, mono equal; the look-ahead scan measured the other way,
+// tools/tune/tune_scan.hip "div" variants)
 template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, int WG = kWG,
-          bool RC = true>
+          bool RC = true, int DV = (sizeof(T) == 2 ? 1 : 0)>
 int launch_tile_scan(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
   constexpr int TF = WG * F * U;
   constexpr int NSEG = U * (WG / 64);
@@ -168,9 +172,9 @@ int launch_tile_scan(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
   if (p.ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
+             "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dv=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
              "remap=%d",
-             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC,
+             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC, DV,
              p.ntiles, WG, lds, TF, xcd_remap);
     return MAVG_OK;
   }
@@ -178,12 +182,12 @@ int launch_tile_scan(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
     static std::once_flag once;
     static hipError_t attr = hipSuccess;
     std::call_once(once, [] {
-      attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_scan_kernel<T, A, C, F, U, HS, NT, WG, RC>),
+      attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_scan_kernel<T, A, C, F, U, HS, NT, WG, RC, DV>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_budget(WG));
     });
     if (attr != hipSuccess) return MAVG_ERR_HIP;
   }
-  hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, WG, RC>), dim3((unsigned)p.ntiles), dim3(WG), lds, st,
+  hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, WG, RC, DV>), dim3((unsigned)p.ntiles), dim3(WG), lds, st,
                      p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
@@ -193,31 +197,33 @@ int launch_tile_scan(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
 // tile t with its carry from earlier records (mavg_lookback.hpp).
 // Workspace: the granule block, at the start of the workspace, padded to
 // 16 bytes (the memset's fast form, cdna_hip_programming.md Guideline 16).
-constexpr int kAheadSlots = 512;  // D: dispatch slots between a record's producer and its tile (multiple of 8)
 constexpr int kAheadSpin = 256;   // polls of an untagged granule before recomputing it
 // Test hook (mavg_test_ahead_schedule): the parity tests force the
 // recompute path with spin 0 and short or absent look-ahead; results are
-// bitwise the same for every setting.  -1 = the constants above.  Relaxed
+// bitwise the same for every setting.  -1 = the tuned defaults.  Relaxed
 // atomics: no environment reads on the launch path.
 extern std::atomic<int> g_test_ahead_slots;
 extern std::atomic<int> g_test_ahead_spin;
 template <typename T, typename A, int C, int F, int U>
-constexpr size_t ahead_granule_bytes(long long nfull) {
+constexpr size_t ahead_granule_bytes(long long nrec) {
   using SA = typename ScanAcc<T, A>::type;
   // + 16 bytes of launch statistics (MAVG_AHEAD_STATS builds only)
-  return (((size_t)(nfull > 0 ? nfull : 1) * C * GranCount<SA>::n * 8) + 15) / 16 * 16 + 16;
+  return (((size_t)(nrec > 0 ? nrec : 1) * C * GranCount<SA>::n * 8) + 15) / 16 * 16 + 16;
 }
-template <typename T, typename A, int C, int F, int U, int NT = kNtStore, int ORD = 2, bool RC = false, int WPS = 1,
-          int PF = 0>
-int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead = -1, int spin = -1) {
+// ahead: D, the dispatch slots between a record's producer and its tile (a
+// multiple of 8; the test hook overrides it)
+template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0>
+int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
   const long long nframes = sg.nframes;
-  if (ahead < 0) {
+  {
     const int t = g_test_ahead_slots.load(std::memory_order_relaxed);
-    ahead = (t >= 0 ? t : kAheadSlots) & ~7;
+    if (t >= 0) ahead = t;
+    ahead &= ~7;
   }
-  if (spin < 0) {
+  int spin = kAheadSpin;
+  {
     const int t = g_test_ahead_spin.load(std::memory_order_relaxed);
-    spin = t >= 0 ? t : kAheadSpin;
+    if (t >= 0) spin = t;
   }
   constexpr int xcd_remap = 1;  // one run per XCD (see ahead_scan_kernel)
   constexpr int TF = kWG * F * U;
@@ -228,20 +234,15 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   const long long ntiles = (nframes + TF - 1) / TF;
   const long long nfull = nframes / TF;
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
-  const size_t need = ahead_granule_bytes<T, A, C, F, U>(nfull);
-  // PF = 0: 4 prefetched record rounds when a window spans more than one
-  // round of kWG records (one per whole tile: k / T + 1) or C == 1, else 1
-  const long long max_records = (long long)k / TF + 1;
-  // mono also below one round: 4 measured faster (fp32 k=8192 0.72 vs 0.69,
-  // int16 k=30000 0.56 vs 0.53); stereo 1 (0.59 vs 0.575, sweep_records.sh)
-  const int pf = PF != 0 ? PF : (max_records > kWG || C == 1 ? 4 : 1);
+  const size_t need = ahead_granule_bytes<T, A, C, F, U>(nfull * (WREC ? kNW : 1));
   const size_t lds = kStageBytes + (size_t)kNW * C * sizeof(A) + (size_t)(NSEG + 3 * kNW) * C * sizeof(SA);
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d,pf=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
-             "ahead=%d remap=%d ws=%zu",
-             type_name<T>(), type_name<A>(), C, F, U, NT, pf, ntiles, kWG, lds, TF, ahead, xcd_remap, need);
+             "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d,rc=%d,dma=%d,wrec=%d,dv=%d> grid=%lld block=%d lds=%zu "
+             "tile_frames=%d ahead=%d remap=%d ws=%zu",
+             type_name<T>(), type_name<A>(), C, F, U, NT, (int)RC, (int)DMA, (int)WREC, DV, ntiles, kWG, lds, TF,
+             ahead, xcd_remap, need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -266,13 +267,30 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.spin = spin;
   p.gran = static_cast<unsigned long long*>(ws.ptr);
   p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
-  if (pf == 4)
-    hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, ORD, RC, WPS, 4>), dim3((unsigned)ntiles), dim3(kWG), lds,
-                       st, p);
-  else
-    hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, ORD, RC, WPS, 1>), dim3((unsigned)ntiles), dim3(kWG), lds,
-                       st, p);
+  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV>), dim3((unsigned)ntiles), dim3(kWG), lds, st,
+                     p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+}
+
+// The look-ahead scan's shape for the dtype, channel count and window
+// (tools/tune/sweep_long.sh, 2^30 samples, k=44100): 4096-frame
+// tiles (U=4 x 16-B units), LDS-DMA stage, non-temporal stage loads and
+// output stores (nt=9).
+//   mono (fp32, int16): per-wave records published early (WREC) while a
+//     window's records fit one round of loads (k/T < 64), D = 512 slots;
+//     fp32 keeps the tile in registers across the second barrier (RC, fewer
+//     live fp64 accumulators)
+//   otherwise: per-tile records, D = 768 (stereo int16) / 1024
+template <typename T, typename A, int C, int F>
+int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
+  constexpr int U = 4;
+  constexpr int TF = kWG * F * U;
+  constexpr int kNtA = kNtStore | kNtHalo;
+  constexpr bool kRC = sizeof(T) == 4 && C == 1;
+  if constexpr (C == 1) {
+    if ((long long)k / TF + 1 <= kWG / kNW) return launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true>(sg, k, st, ws, 512);
+  }
+  return launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false>(sg, k, st, ws, C == 2 ? 768 : 1024);
 }
 
 // segment streaming with the launch geometry measured best: short
@@ -307,8 +325,7 @@ bool segment_ring_fits(int k) {
 //     fp32   mono H <= 512: U2 nt rc | H <= 4 KiB: U2 ntS rc | H <= 8 KiB: U2 x 512 ntS rc |
 //            H <= 16 KiB: U4 x 512 ntS rc
 //     longer windows (fp32 H > 16 KiB, int16 past the 1024-thread tile): the
-//     look-ahead scan, U4, nt output stores (needs the workspace); 0.69-0.73
-//     of peak whatever k (tools/tune/sweep_ahead.sh)
+//     look-ahead scan (dispatch_ahead; needs the workspace)
 //   Hillis-Steele flavour: the halo-staged tile while it fits LDS (fp32: U4 nt
 //   for H <= 512 B, else U8 ntS; int16: U4 x 512 threads ntS), then the
 //   segment-streaming scan.
@@ -368,7 +385,7 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
       // fp32 halos past 16 KiB: the look-ahead scan beats the 1024-thread
       // tile (k=8192: 0.73 vs 0.69; k=12000: 0.71 vs 0.64, sweep_ahead.sh)
     }
-    return launch_ahead_scan<T, A, C, F, 4, kNtStore>(sg, k, st, ws);
+    return dispatch_ahead<T, A, C, F>(sg, k, st, ws);
   } else {
     // Hillis-Steele: the element-wise log-step scans make a tile's compute
     // long, so bigger tiles (fewer halos and barriers per byte) and the split

@@ -92,6 +92,18 @@ __device__ __forceinline__ void stage_shifted_tile(const T* __restrict__ in, con
 // HBM traffic is the algorithmic 8 B/sample (fp32) plus the granules; the
 // second read of each tile is served by L2 / MALL.
 //
+// Round 2 (this form): the shifted tile reaches LDS by LDS-DMA
+// (global_load_lds_dwordx4, no staging registers); the partial window (the
+// k mod T frames before the window's first whole tile) is summed from the
+// x[n-k] units the in-tile scan reads anyway -- they are exactly those frames
+// -- instead of an element-wise LDS sweep; the rare paths (head duty, record
+// recompute, edge tiles) load one unit at a time so they do not set the
+// register allocation (fp32 106 -> 80-90 VGPRs, int16 86-91 -> 69-74); and
+// (WREC) each wave publishes its own share of a record as soon as it is
+// summed, phase A's loads issued first, so records appear earlier in the
+// producer's life and the look-ahead distance can stay short enough for the
+// prefetched tiles to survive in the XCD's 4 MB L2.
+//
 // Progress never depends on scheduling: a granule still untagged after a
 // bounded number of polls is recomputed by the waiting wave from the input
 // with the producer's lane mapping and order of operations, so the value --
@@ -182,14 +194,51 @@ struct AheadParams {
   OutParams o;
 };
 
-// ORD: 0 = phase A, then the tile and the stage; 1 = phase A loads, tile
-// loads, phase A record, stage; 2 = tile, stage and phase A loads all in
-// flight, then the stage stores and the phase A record
-// PF: rounds of WG records whose loads are all issued before the barrier
-// (1, or 4 for windows spanning more than WG records: the rounds are then not
-// a chain of dependent L2 round trips)
-template <typename T, typename A, int C, int F, int U, int NT, int ORD = 2, bool RC = false, int WPS = 1, int PF = 1>
-__global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
+// One 16-B LDS-DMA load per lane (global_load_lds_dwordx4): lane l's 16 bytes
+// land at lds_wave + 16 l; lds_wave must be wave-uniform (it goes to M0).
+// NT: non-temporal (aux = 2).
+template <bool NT = false>
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave, 16, 0, NT ? 2 : 0);
+}
+
+// wave_record (mavg_lookback.hpp) with one unit in registers at a time: the
+// same additions in the same order, so the same bits.  For the rare paths.
+template <typename T, typename SA, int C, int F, int U, int WG>
+__device__ __forceinline__ void wave_record_lean(const T* __restrict__ in, long long j, int wv, int lane, bool eio,
+                                                 SA (&r)[C]) {
+  constexpr int VE = F * C;
+  constexpr int TF = WG * F * U;
+  using IO = UnitIO<T, VE>;
+  SA ls[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) ls[c] = (SA)0;
+#pragma unroll 1
+  for (int u = 0; u < U; ++u) {
+    const Unit<T, VE> xu = IO::gload(in + (j * TF + (long long)(u * WG + wv * 64 + lane) * F) * C, eio);
+#pragma unroll
+    for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+      for (int c = 0; c < C; ++c) ls[c] += to_acc<SA>(xu.e[fr * C + c]);
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) r[c] = readlane(wave_incl_scan(ls[c]), 63);
+}
+
+// RC: keep the own tile's registers (U*F*C samples) across the second barrier
+//     and rebuild the in-lane prefix at the output from them and the stage,
+//     instead of keeping U*F*C accumulators (fewer registers for fp32, whose
+//     accumulators are fp64; the same additions in the same order).
+// DMA: stage interior shifted tiles by LDS-DMA (16-B units only).
+// DV: the int16 output division (to_out: 0 fp64 product, 1 magic multiply).
+// WREC: one record per (tile, wave) instead of per tile, each published by its
+//     wave as soon as its share is summed (no barrier before publication; phase
+//     A's loads are issued first), so records appear earlier in the producer's
+//     life; consumers read NW times as many granules.
+template <typename T, typename A, int C, int F, int U, int NT, bool RC = false, bool DMA = true, bool WREC = false,
+          int DV = 0>
+__global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
   constexpr int WG = kWG;
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
@@ -201,6 +250,7 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   using U_t = Unit<T, VE>;
   using SA = typename ScanAcc<T, A>::type;
   constexpr int NG = GranCount<SA>::n;
+  constexpr bool kDma = DMA && IO::kVec && VE * (int)sizeof(T) == 16;
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* stage = reinterpret_cast<T*>(smem);
@@ -215,6 +265,7 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = tid >> 6;
+  const int wq = __builtin_amdgcn_readfirstlane(w);
   const int k = p.k;
   const long long nframes = p.nframes;
   const int pre = p.pre;
@@ -225,79 +276,90 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   const int Ha = p.halo_units * F;
   const long long h0 = t0 - Ha;
   const bool tile_full = (t0 + TF <= nframes);
-  const long long a = t0 - k;
-  const long long jlo = a >= 0 ? (a + TF - 1) / TF : 0;
-  const long long qlo = jlo, qhi = tile;  // records of the whole tiles [jlo, tile)
+  const long long a = t0 - k;                                   // first frame of the window before t0
+  const long long jlo = a >= 0 ? (a + TF - 1) / TF : 0;         // first whole tile inside it
+  constexpr int RPT = WREC ? NW : 1;                            // records per tile
+  const long long qlo = jlo * RPT, qhi = tile * RPT;            // records of the whole tiles [jlo, tile)
+  const int pcount = a >= 0 ? (int)(jlo * TF - a) : 0;          // window frames before tile jlo (< TF)
 
-  // ---- phase A (this wave's share of tile t + D -> record) and phase B's
-  //      loads: the tile (an L2 / MALL hit: phase A of tile t-D) and the
-  //      shifted tile ----
+  // ---- 1. loads: the tile, the shifted tile, phase A's tile (tile t + D:
+  //         default policy, it stays in L2), then the first round of records
+  //         (as late as possible: a record read early may not be published yet) ----
   const unsigned nb = gridDim.x;
   const unsigned bd = blockIdx.x + (unsigned)p.ahead;  // the block D dispatch slots later (same XCD)
   const long long ja = bd < nb ? remap_tile(bd, nb, p.xcd_remap) : -1;
   const bool produce = ja >= 0 && ja < p.nfull;
   U_t xa[U];
-  auto load_a = [&]() {
+  if constexpr (WREC) {  // phase A's loads first: the HBM fetch with the longest latency
     if (produce)
 #pragma unroll
       for (int u = 0; u < U; ++u) xa[u] = IO::gload(in + (ja * TF + (long long)(u * WG + tid) * F) * C, eio);
-  };
-  // source 0 = phase A (tile ja), 1 = own tile, 2 = head duty: each wave
-  // leaves its share in LDS, published after the first barrier
-  auto share = [&](int src, const SA (&r)[C]) {
-    if (lane == 0)
-#pragma unroll
-      for (int c = 0; c < C; ++c) shares[(src * NW + w) * C + c] = r[c];
-  };
-  auto publish_a = [&]() {
-    if (produce) {
-      SA r[C];
-      wave_record<T, SA, C, F, U>(xa, r);
-      share(0, r);
-    }
-  };
+  }
   U_t x[U];
-  auto load_tile = [&]() {
+  if (tile_full) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      x[u] = IO::template gload<(NT & kNtLoad) != 0>(in + (t0 + (long long)(u * WG + tid) * F) * C, eio);
+  } else {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long f = t0 + (long long)(u * WG + tid) * F;
-      if (tile_full) {
-        x[u] = IO::template gload<(NT & kNtLoad) != 0>(in + f * C, eio);
-      } else {
 #pragma unroll
-        for (int fr = 0; fr < F; ++fr)
+      for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-          for (int c = 0; c < C; ++c) x[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k, pre);
-      }
+        for (int c = 0; c < C; ++c) x[u].e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k, pre);
+    }
+  }
+  const bool stage_fast = !eio && h0 >= 0 && h0 + (long long)kStageUnits * F <= nframes;
+  if (kDma && stage_fast) {
+    if constexpr (kDma) {
+      unsigned char* sb = reinterpret_cast<unsigned char*>(stage);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        glds16<(NT & kNtHalo) != 0>(in + (h0 + (long long)(u * WG + tid) * F) * C, sb + (u * WG + wq * 64) * 16);
+      if (tid == 0) glds16<(NT & kNtHalo) != 0>(in + (h0 + (long long)(U * WG) * F) * C, sb + (U * WG) * 16);
+    }
+  } else if (stage_fast) {  // register staging (units that are not 16 B)
+    stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, pre, eio, tid);
+  } else {  // edge tiles: guarded, one unit at a time
+#pragma unroll 1
+    for (int j = tid; j < kStageUnits; j += WG) {
+      const long long f = h0 + (long long)j * F;
+      U_t h;
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c) h.e[fr * C + c] = load_elem(in, hist, f + fr, c, C, nframes, k, pre);
+      IO::store(stage + j * VE, h);
+    }
+  }
+  // a wave's share of a record: kept in LDS for the block's publication
+  // after the first barrier, or (WREC) published by the wave itself now
+  auto share = [&](int src, long long j, const SA (&r)[C]) {
+    if constexpr (WREC) {
+      publish_record<SA, C>(gran, j * NW + w, r, lane);
+    } else if (lane == 0) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) shares[(src * NW + w) * C + c] = r[c];
     }
   };
-  if constexpr (ORD == 0) {
-    load_a();
-    publish_a();
-    load_tile();
-    stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, pre, eio, tid);
-  } else if constexpr (ORD == 1) {
-    load_a();
-    load_tile();
-    publish_a();
-    stage_shifted_tile<T, C, F, U, WG, NT>(in, hist, stage, h0, nframes, k, pre, eio, tid);
-  } else {
-    U_t hs[U + 1];
-    load_tile();
-    stage_shifted_load<T, C, F, U, WG, NT>(in, hist, hs, h0, nframes, k, pre, eio, tid);
-    load_a();
-    stage_shifted_store<T, C, F, U, WG>(stage, hs, tid);
-    publish_a();
+  if (produce) {
+    if constexpr (!WREC)
+#pragma unroll
+      for (int u = 0; u < U; ++u) xa[u] = IO::gload(in + (ja * TF + (long long)(u * WG + tid) * F) * C, eio);
+    SA r[C];
+    wave_record<T, SA, C, F, U>(xa, r);
+    share(0, ja, r);
   }
   const bool own = blockIdx.x < (unsigned)p.ahead && tile < p.nfull;  // no block D slots earlier
   if (own) {
     SA r[C];
     wave_record<T, SA, C, F, U>(x, r);
-    share(1, r);
+    share(1, tile, r);
   }
   // head duty (remap mode 1): the first tiles of XCD run x need the records of
-  // the last tiles of run x-1, whose blocks are dispatched at the end of the
-  // grid; the first `head` blocks of run x publish those records instead
+  // the last tiles of run x-1, dispatched at the end of the grid; the first
+  // `head` blocks of run x publish those
   long long jh = -1;
   if (p.xcd_remap == 1) {
     const unsigned xr = blockIdx.x & 7u, s = blockIdx.x >> 3;
@@ -307,27 +369,22 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
     }
   }
   if (jh >= 0) {
-    U_t xh[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) xh[u] = IO::gload(in + (jh * TF + (long long)(u * WG + tid) * F) * C, eio);
     SA r[C];
-    wave_record<T, SA, C, F, U>(xh, r);
-    share(2, r);
+    wave_record_lean<T, SA, C, F, U, WG>(in, jh, w, lane, eio, r);
+    share(2, jh, r);
   }
-  // first PF rounds of record loads (checked after the in-tile scan)
-  unsigned long long rvp[PF][C][NG];
-#pragma unroll
-  for (int r = 0; r < PF; ++r) {
-    const long long q = qlo + (long long)r * WG + tid;
+  unsigned long long rv[C][NG];
+  {
+    const long long q = qlo + tid;
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int h = 0; h < NG; ++h) rvp[r][c][h] = q < qhi ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
+      for (int h = 0; h < NG; ++h) rv[c][h] = q < qhi ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
   }
   __syncthreads();
   // publish the records whose wave shares this block holds: wave src adds
   // source src's NW shares in wave order
-  if (w < 3) {
+  if (!WREC && w < 3) {
     const long long j = w == 0 ? (produce ? ja : -1) : (w == 1 ? (own ? tile : -1) : jh);
     if (j >= 0) {
       SA r[C];
@@ -341,27 +398,20 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
     }
   }
 
-  // ---- partial carry: the part of [a, t0) before the first whole tile ----
+  // ---- 2. the carry's partial window: frames [a, jlo*T), which are the
+  //         x[n-k] of this tile's first pcount frames (added in the scan below);
+  //         before frame 0 (a < 0): history and/or the peeled head ----
   A hp[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) hp[c] = (A)0;
-  if (a >= 0) {
-    const int pcount = (int)(jlo * TF - a);
-    const int s0 = Ha - k;
-    for (int i = tid; i < pcount; i += WG)
-#pragma unroll
-      for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(stage[(s0 + i) * C + c]);
-  } else if (hist != nullptr || pre > 0) {  // frames before 0: history and/or the peeled head
+  if (a < 0 && (hist != nullptr || pre > 0)) {
+#pragma unroll 1
     for (long long f = a + tid; f < 0; f += WG)
 #pragma unroll
       for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(load_elem(in, hist, f, c, C, nframes, k, pre));
   }
 
-  // ---- d = x - x[n-k]; in-lane, wave and segment scans ----
-  // RC: only each lane's total crosses the second barrier; the in-lane
-  // prefix is rebuilt afterwards from x (registers) and the stage, in the
-  // same order, so the outputs are bitwise the same with U*F*C fewer live
-  // accumulators (as in tile_scan_kernel)
+  // ---- 3. d = x - x[n-k]; in-lane, wave and segment scans ----
   auto stage_xk = [&](int j) -> U_t {
     const int e = (Ha + j * F - k) * C;  // stage element of x[n-k]
     U_t xk;
@@ -385,6 +435,19 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const U_t xk = stage_xk(u * WG + tid);
+    const int f0 = (u * WG + tid) * F;
+    if (f0 + F <= pcount) {
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+        for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(xk.e[fr * C + c]);
+    } else if (f0 < pcount) {
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr)
+        if (f0 + fr < pcount)
+#pragma unroll
+          for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(xk.e[fr * C + c]);
+    }
     SA run[C];
     if constexpr (RC) {
 #pragma unroll
@@ -413,67 +476,62 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
     }
   }
 
-  // ---- whole-tile carry from the records (rounds of WG records) ----
+  // ---- 4. whole-tile carry from the records, WG per round ----
   A hq[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) hq[c] = (A)0;
-  int ri = 0;
-  for (long long qb = qlo; qb < qhi; qb += WG, ++ri) {
+#pragma unroll 1
+  for (long long qb = qlo; qb < qhi; qb += WG) {
     const long long q = qb + tid;
     const bool act = q < qhi;
-    unsigned long long rv[C][NG];
-    if (ri < PF) {
-#pragma unroll
-      for (int r = 0; r < PF; ++r)  // static register selection, no indexed scratch
-        if (r == ri)
-#pragma unroll
-          for (int c = 0; c < C; ++c)
-#pragma unroll
-            for (int h = 0; h < NG; ++h) rv[c][h] = rvp[r][c][h];
-    } else {
+    if (qb != qlo) {
 #pragma unroll
       for (int c = 0; c < C; ++c)
 #pragma unroll
         for (int h = 0; h < NG; ++h) rv[c][h] = act ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
-    }
-    for (int it = 0;; ++it) {
-      bool miss = false;
-#pragma unroll
-      for (int c = 0; c < C; ++c)
-#pragma unroll
-        for (int h = 0; h < NG; ++h) miss |= act && (rv[c][h] >> 32) != 1ull;
-      if (!__any(miss) || it >= p.spin) break;
-#ifdef MAVG_AHEAD_STATS
-      if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats) + 1, 1u);
-#endif
-      __builtin_amdgcn_s_sleep(2);
-      if (miss)
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-#pragma unroll
-          for (int h = 0; h < NG; ++h) rv[c][h] = gran_load(gran + (q * C + c) * NG + h);
     }
     bool miss = false;
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int h = 0; h < NG; ++h) miss |= act && (rv[c][h] >> 32) != 1ull;
-    // still untagged: the wave recomputes each such record from the input
+#pragma unroll 1
+    for (int it = 0; __any(miss) && it < p.spin; ++it) {
+#ifdef MAVG_AHEAD_STATS
+      if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats) + 1, 1u);
+#endif
+      __builtin_amdgcn_s_sleep(2);
+      if (miss) {
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+          for (int h = 0; h < NG; ++h) rv[c][h] = gran_load(gran + (q * C + c) * NG + h);
+      }
+      miss = false;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int h = 0; h < NG; ++h) miss |= act && (rv[c][h] >> 32) != 1ull;
+    }
+    // still untagged: the wave recomputes each such record from the input,
+    // with the producer's lane mapping and order of operations
     unsigned long long mask = __ballot(miss);
+#pragma unroll 1
     while (mask != 0ull) {
       const int l = __builtin_ctzll(mask);
       mask &= mask - 1ull;
-      const long long jj = __shfl(q, l, 64);  // the tile whose record is missing
+      const long long jj = __shfl(q, l, 64);
       SA r[C];
-      for (int wv = 0; wv < NW; ++wv) {  // its NW wave shares, in wave order
-        U_t xr[U];
+      if constexpr (WREC) {  // record jj = (tile, wave)
+        wave_record_lean<T, SA, C, F, U, WG>(in, jj / NW, (int)(jj % NW), lane, eio, r);
+      } else {
+#pragma unroll 1
+        for (int wv = 0; wv < NW; ++wv) {
+          SA rw[C];
+          wave_record_lean<T, SA, C, F, U, WG>(in, jj, wv, lane, eio, rw);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          xr[u] = IO::gload(in + (jj * TF + (long long)(u * WG + wv * 64 + lane) * F) * C, eio);
-        SA rw[C];
-        wave_record<T, SA, C, F, U>(xr, rw);
-#pragma unroll
-        for (int c = 0; c < C; ++c) r[c] = wv == 0 ? rw[c] : r[c] + rw[c];
+          for (int c = 0; c < C; ++c) r[c] = wv == 0 ? rw[c] : r[c] + rw[c];
+        }
       }
       if (lane == l)
 #pragma unroll
@@ -500,23 +558,24 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
   }
   __syncthreads();
 
-  // ---- carry + earlier segments; outputs ----
+  // ---- 5. carry + earlier segments; outputs ----
   static_assert(NSEG <= 64, "segment totals are scanned across one wave");
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  A base[U][C];
+  A w0[C];
+  SA ex[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    A w0 = (A)0;
+    w0[c] = (A)0;
 #pragma unroll
-    for (int i = 0; i < NW; ++i) w0 += hsum[i * C + c];
+    for (int i = 0; i < NW; ++i) w0[c] += hsum[i * C + c];
     const SA tv = lane < NSEG ? tot[lane * C + c] : (SA)0;
-    const SA ex = wave_incl_scan(tv) - tv;
-#pragma unroll
-    for (int u = 0; u < U; ++u) base[u][c] = w0 + (A)readlane(ex, u * NW + wu);
+    ex[c] = wave_incl_scan(tv) - tv;
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const long long f = t0 + (long long)(u * WG + tid) * F;
+    A b[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) b[c] = w0[c] + (A)(readlane(ex[c], u * NW + wq) + lx[u][c]);
     U_t y;
     if constexpr (RC) {
       const U_t xk = stage_xk(u * WG + tid);
@@ -528,14 +587,13 @@ __global__ __launch_bounds__(kWG, WPS) void ahead_scan_kernel(AheadParams p) {
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           run[c] += to_acc<SA>(x[u].e[fr * C + c]) - to_acc<SA>(xk.e[fr * C + c]);
-          y.e[fr * C + c] = to_out<T, A>(base[u][c] + (A)(lx[u][c] + run[c]), p.o);
+          y.e[fr * C + c] = to_out<T, A, DV>(b[c] + (A)run[c], p.o);
         }
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-        for (int c = 0; c < C; ++c)
-          y.e[fr * C + c] = to_out<T, A>(base[u][c] + (A)(lx[u][c] + v[u][fr][c]), p.o);
+        for (int c = 0; c < C; ++c) y.e[fr * C + c] = to_out<T, A, DV>(b[c] + (A)v[u][fr][c], p.o);
     }
     if (tile_full) {
       IO::template gstore<(NT & kNtStore) != 0>(out + f * C, y, eio);

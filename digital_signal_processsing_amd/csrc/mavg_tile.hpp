@@ -48,7 +48,7 @@ struct TileParams {
 //     (the tile and x[n-k] are both staged), in the same order, so the
 //     outputs are bitwise the same with U*F*C fewer live accumulators.
 template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, int WG = kWG,
-          bool RC = true>
+          bool RC = true, int DV = 0>
 __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
         const long long f = sb + r * 64 + lane;
         if (tile_full || f < nframes)
 #pragma unroll
-          for (int c = 0; c < C; ++c) out[f * C + c] = to_out<T, A>(base[u][c] + v[u][r][c], p.o);
+          for (int c = 0; c < C; ++c) out[f * C + c] = to_out<T, A, DV>(base[u][c] + v[u][r][c], p.o);
       }
       continue;
     }
@@ -272,13 +272,13 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           run[c] += to_acc<A>(xu.e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
-          y.e[fr * C + c] = to_out<T, A>(base[u][c] + lx[u][c] + run[c], p.o);
+          y.e[fr * C + c] = to_out<T, A, DV>(base[u][c] + lx[u][c] + run[c], p.o);
         }
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)
 #pragma unroll
-        for (int c = 0; c < C; ++c) y.e[fr * C + c] = to_out<T, A>(base[u][c] + lx[u][c] + v[u][fr][c], p.o);
+        for (int c = 0; c < C; ++c) y.e[fr * C + c] = to_out<T, A, DV>(base[u][c] + lx[u][c] + v[u][fr][c], p.o);
     }
     if (tile_full) {
       IO::template gstore<(NT & kNtStore) != 0>(out + f * C, y, eio);

@@ -121,8 +121,10 @@ def test_plan_describes_launch_without_gpu():
 def test_workspace_only_for_ahead_scan():
     import digital_signal_processsing_amd as dsp
     # halo-staged tiles need none; the look-ahead scan needs its record
-    # granules: 8 bytes per (whole tile, channel, 32-bit word of the tile-sum
-    # type), padded to 16 bytes, plus 16 bytes of statistics
+    # granules: 8 bytes per (record, channel, 32-bit word of the tile-sum
+    # type), padded to 16 bytes, plus 16 bytes of statistics; a record per
+    # whole tile, or per (whole tile, wave) -- 4 per tile -- for mono windows
+    # whose records fit one round of loads (WREC)
     assert dsp.workspace_bytes(1 << 30, 1024) == 0
     assert dsp.workspace_bytes(1 << 30, 4096) == 0
     # fp32 halos past 16 KiB take the look-ahead scan (U=4: 4096-frame tiles);
@@ -130,10 +132,11 @@ def test_workspace_only_for_ahead_scan():
     # which a view that is not 16-B aligned may run
     tiles = (1 << 30) // 4096
     assert dsp.plan(1 << 30, 8192).startswith("ahead_scan<f32,acc=f64,C=1,F=4,U=4")
-    assert "ws=%d" % (tiles * 2 * 8 + 16) in dsp.plan(1 << 30, 20_000)
+    assert "wrec=1" in dsp.plan(1 << 30, 20_000) and "ws=%d" % (tiles * 4 * 2 * 8 + 16) in dsp.plan(1 << 30, 20_000)
+    assert "wrec=0" in dsp.plan(1 << 30, 300_000) and "ws=%d" % (tiles * 2 * 8 + 16) in dsp.plan(1 << 30, 300_000)
     assert dsp.plan(1 << 30, 8192, algo="blelloch_scalar").startswith("ahead_scan<f32,acc=f64,C=1,F=1,U=4")
-    assert dsp.workspace_bytes(1 << 30, 8192) == 4 * tiles * 2 * 8 + 16
-    assert dsp.workspace_bytes(1 << 30, 8192, algo="blelloch_scalar") == 4 * tiles * 2 * 8 + 16
+    assert dsp.workspace_bytes(1 << 30, 8192) == 4 * tiles * 4 * 2 * 8 + 16
+    assert dsp.workspace_bytes(1 << 30, 8192, algo="blelloch_scalar") == 4 * tiles * 4 * 2 * 8 + 16
     assert dsp.plan(1 << 30, 8192, algo="hillis").startswith("segment_scan<")
     # int16 keeps the 1024-thread tile up to ~47 KiB of halo
     assert dsp.workspace_bytes(1 << 30, 8192, dtype=dsp.I16) == 0

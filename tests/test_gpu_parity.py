@@ -418,9 +418,10 @@ def test_ahead_records_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, 
     frames = 2_600_000 // C + 12_345  # > D = 512 tiles at C=1: the look-ahead producers run
     plan = dsp.plan(frames * C, k, C, dt)
     assert plan.startswith("ahead_scan<")
-    # mono, and windows of more than 256 records, take the prefetched-rounds form
+    # mono windows whose per-wave records fit one round of loads take the
+    # per-wave records (wrec=1); the others one record per tile
     tf = int(plan.split("tile_frames=")[1].split()[0])
-    assert ("pf=4" in plan) == (C == 1 or k // tf + 1 > 256), plan
+    assert ("wrec=1" in plan) == (C == 1 and k // tf + 1 <= 64), plan
     if dtype == "f32":
         x = oracle_mod.synth_f32(frames * C, seed=77, dist=1)
     else:

@@ -14,20 +14,26 @@ sys.path.insert(0, ROOT)
 import pmc_traffic  # noqa: E402
 
 
+def latest_trace_summary():
+    """The newest round's kernel trace summary under profiles/ (rNN_...)."""
+    import glob
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_trace_summary.csv")))[-1]
+
+
 def test_kernel_key_parses_rocprof_names():
-    name = "void mavg::ahead_scan_kernel<float, double, 1, 4, 4, 1, 2, false, 1, 4>(mavg::AheadParams)"
+    name = "void mavg::ahead_scan_kernel<float, double, 1, 4, 4, 9, true, true, true, 0>(mavg::AheadParams)"
     assert pmc_traffic.kernel_key(name) == ("ahead_scan_kernel",
-                                            ("float", "double", "1", "4", "4", "1", "2", "false", "1", "4"))
+                                            ("float", "double", "1", "4", "4", "9", "true", "true", "true", "0"))
     assert pmc_traffic.kernel_key("__amd_rocclr_fillBufferAligned") is None
 
 
 def test_every_bench_workload_matches_a_traced_kernel():
-    """Each workload's plan maps to a kernel signature present in the
-    committed kernel trace summary (profiles/r01_kernel_trace_summary.csv)."""
+    """Each workload's plan maps to a kernel signature present in the newest
+    committed kernel trace summary (profiles/rNN_kernel_trace_summary.csv)."""
     import bench
     import digital_signal_processsing_amd as dsp
     traced = set()
-    with open(os.path.join(ROOT, "profiles", "r01_kernel_trace_summary.csv")) as f:
+    with open(latest_trace_summary()) as f:
         for row in csv.DictReader(f):
             kk = pmc_traffic.kernel_key(row["kernel"])
             if kk is not None:

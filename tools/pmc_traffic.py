@@ -50,11 +50,13 @@ def plan_key(plan):
     hs = "true" if flavour and flavour[0] == "hillis" else "false"
     wg = re.search(r"block=(\d+)", plan).group(1)
     if fam == "tile_scan":
-        args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["nt"], wg, "true" if kv.get("rc", "1") == "1" else "false")
+        args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["nt"], wg, "true" if kv.get("rc", "1") == "1" else "false",
+                kv.get("dv", "0"))
     elif fam == "direct":
         args = (T, acc, kv["C"], kv["F"], kv["U"], wg)
-    elif fam == "ahead_scan":  # ORD=2, RC=false, WPS=1 (the dispatch's only choice); PF from the plan
-        args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], "2", "false", "1", kv.get("pf", "1"))
+    elif fam == "ahead_scan":
+        b = {"0": "false", "1": "true"}
+        args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], b[kv["rc"]], b[kv["dma"]], b[kv["wrec"]], kv["dv"])
     elif fam == "segment_scan":
         args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["pd"], kv["nt"])
     else:

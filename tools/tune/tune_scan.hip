@@ -15,9 +15,6 @@
 #include <vector>
 
 #include "../../digital_signal_processsing_amd/csrc/mavg_launch.hpp"
-#include "twopass_experiment.hpp"
-#include "onepass_experiment.hpp"
-#include "ahead_wave_records.hpp"
 
 using namespace mavg;
 
@@ -164,7 +161,7 @@ int run(int lg, int k, int rounds) {
       CK(hipMemcpyAsync(&v.mism, dcnt, 8, hipMemcpyDeviceToHost, st));
     }
     CK(hipStreamSynchronize(st));
-    if (v.name.find("ahead") != std::string::npos) {
+    if (v.name.find("ahead") != std::string::npos && v.name.find("product") == std::string::npos) {
       LaunchPlan lp{};
       g_plan = &lp;
       v.launch(st);
@@ -214,42 +211,42 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   vs.push_back({"scan U" #U " PD" #PD " NT" #NT " ov" #OV, true, [=](hipStream_t s) {                       \
                   ScanTuning t;                                                                             \
                   t.oversub = OV;                                                                           \
-                  return launch_scan<float, double, 1, 4, U, false, PD, NT>(x, y, nullptr, n, k, s, t);     \
+                  return launch_scan<float, double, 1, 4, U, false, PD, NT>(Sig{x, y, nullptr, n}, k, s, t);     \
                 }});
   SCAN(2, 2, 3, 1)
 #define TILE(U, NT, RM)                                                                                  \
   vs.push_back({"tile U" #U " NT" #NT " remap" #RM, true, [=](hipStream_t s) {                             \
-                  return launch_tile_scan<float, double, 1, 4, U, false, NT>(x, y, nullptr, n, k, s, RM);   \
+                  return launch_tile_scan<float, double, 1, 4, U, false, NT>(Sig{x, y, nullptr, n}, k, s, RM);   \
                 }});
 #define DIRECT(U, WG)                                                                                   \
   vs.push_back({"direct U" #U " wg" #WG, true, [=](hipStream_t s) {                                        \
-                  return launch_direct<float, double, 1, 4, U, WG>(x, y, nullptr, n, k, s, 1);             \
+                  return launch_direct<float, double, 1, 4, U, WG>(Sig{x, y, nullptr, n}, k, s, 1);             \
                 }});
 #define TILEW(U, WG)                                                                                    \
   vs.push_back({"tile U" #U " wg" #WG, true, [=](hipStream_t s) {                                         \
-                  return launch_tile_scan<float, double, 1, 4, U, false, 0, WG>(x, y, nullptr, n, k, s, 1); \
+                  return launch_tile_scan<float, double, 1, 4, U, false, 0, WG>(Sig{x, y, nullptr, n}, k, s, 1); \
                 }});
 #define SEGR(U, PD, NT, SC)                                                                              \
   vs.push_back({"seg U" #U " PD" #PD " NT" #NT " sc" #SC " remap", true, [=](hipStream_t s) {              \
                   ScanTuning t;                                                                         \
                   t.seg_chunks = SC;                                                                    \
                   t.xcd_remap = 1;                                                                      \
-                  return launch_scan<float, double, 1, 4, U, false, PD, NT>(x, y, nullptr, n, k, s, t); \
+                  return launch_scan<float, double, 1, 4, U, false, PD, NT>(Sig{x, y, nullptr, n}, k, s, t); \
                 }});
 #define TILEM(U, M)                                                                                     \
   vs.push_back({"tile U" #U " remap" #M, true, [=](hipStream_t s) {                                       \
-                  return launch_tile_scan<float, double, 1, 4, U, false, 0>(x, y, nullptr, n, k, s, M); \
+                  return launch_tile_scan<float, double, 1, 4, U, false, 0>(Sig{x, y, nullptr, n}, k, s, M); \
                 }});
 #define DIRECTM(M)                                                                                      \
   vs.push_back({"direct U1 remap" #M, true, [=](hipStream_t s) {                                          \
-                  return launch_direct<float, double, 1, 4, 1>(x, y, nullptr, n, k, s, M);                 \
+                  return launch_direct<float, double, 1, 4, 1>(Sig{x, y, nullptr, n}, k, s, M);                 \
                 }});
   vs.push_back({"hillis tile U2", true, [=](hipStream_t s) {
-                  return launch_tile_scan<float, double, 1, 4, 2, true, 0>(x, y, nullptr, n, k, s);
+                  return launch_tile_scan<float, double, 1, 4, 2, true, 0>(Sig{x, y, nullptr, n}, k, s);
                 }});
 #define HTS(U, NT, WG)                                                                                  \
   vs.push_back({"hillisS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                              \
-                  return launch_tile_scan<float, double, 1, 4, U, true, NT, WG>(x, y, nullptr, n, k, s);     \
+                  return launch_tile_scan<float, double, 1, 4, U, true, NT, WG>(Sig{x, y, nullptr, n}, k, s);     \
                 }});
   HTS(2, 0, 256)
   HTS(2, 1, 256)
@@ -267,22 +264,22 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   HTS(2, 13, 1024)
   HTS(4, 13, 1024)
   vs.push_back({"hillis tile U1", true, [=](hipStream_t s) {
-                  return launch_tile_scan<float, double, 1, 4, 1, true, 0>(x, y, nullptr, n, k, s);
+                  return launch_tile_scan<float, double, 1, 4, 1, true, 0>(Sig{x, y, nullptr, n}, k, s);
                 }});
 #define TILENR(U, NT)                                                                                   \
   vs.push_back({"tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                                 \
-                  return launch_tile_scan<float, double, 1, 4, U, false, NT, 256, false>(x, y, nullptr, n, k, s); \
+                  return launch_tile_scan<float, double, 1, 4, U, false, NT, 256, false>(Sig{x, y, nullptr, n}, k, s); \
                 }});
   TILENR(2, 0)
   TILENR(4, 3)
   TILENR(8, 0)
 #define TILEWG(U, WG)                                                                                   \
   vs.push_back({"tile U" #U " wg" #WG " rc", true, [=](hipStream_t s) {                                   \
-                  return launch_tile_scan<float, double, 1, 4, U, false, 0, WG>(x, y, nullptr, n, k, s, 64); \
+                  return launch_tile_scan<float, double, 1, 4, U, false, 0, WG>(Sig{x, y, nullptr, n}, k, s, 64); \
                 }});
 #define TILEX(U, NT, WG, RC)                                                                            \
   vs.push_back({"tileX U" #U " nt" #NT " wg" #WG " rc" #RC, true, [=](hipStream_t s) {                    \
-                  return launch_tile_scan<float, double, 1, 4, U, false, NT, WG, RC>(x, y, nullptr, n, k, s, 64); \
+                  return launch_tile_scan<float, double, 1, 4, U, false, NT, WG, RC>(Sig{x, y, nullptr, n}, k, s, 64); \
                 }});
   TILEX(2, 1, 256, false)
   TILEX(2, 0, 512, false)
@@ -308,51 +305,16 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   TILEWG(2, 256)
   TILEWG(2, 512)
   // clean grid for the dispatch rules (tools/tune/sweep_shapes.sh)
-#define LB(U)                                                                                           \
-  vs.push_back({"lookback U" #U, true, [=](hipStream_t s) {                                               \
-                  return launch_lookback_scan<float, double, 1, 4, U, 0>(x, y, nullptr, n, k, s, g_ws);        \
+#define AH2(U, RC, DMA, D, W, NT)                                                                       \
+  vs.push_back({"ahead U" #U " rc" #RC " dma" #DMA " D" #D " w" #W " nt" #NT, true, [=](hipStream_t s) { \
+                  return launch_ahead_scan<float, double, 1, 4, U, NT, RC, DMA, W>(Sig{x, y, nullptr, n}, k, s, g_ws, D); \
                 }});
-  LB(1)
-  LB(2)
-  LB(4)
-#define AH(U, NT, D, ORD, WPS)                                                                          \
-  vs.push_back({"ahead U" #U " nt" #NT " D" #D " o" #ORD " w" #WPS, true, [=](hipStream_t s) {            \
-                  return launch_ahead_scan<float, double, 1, 4, U, NT, ORD, false, WPS>(x, y, nullptr, n, k, s, g_ws, D); \
-                }});
-  AH(4, 1, 512, 2, 1)
-#define AHP(PF)                                                                                         \
-  vs.push_back({"ahead U4 pf" #PF, true, [=](hipStream_t s) {                                             \
-                  return launch_ahead_scan<float, double, 1, 4, 4, 1, 2, false, 1, PF>(x, y, nullptr, n, k, s, g_ws, 512); \
-                }});
-  AHP(1)
-  AHP(4)
-  vs.push_back({"ahead rc pf4", true, [=](hipStream_t s) {
-                  return launch_ahead_scan<float, double, 1, 4, 4, 1, 2, true, 1, 4>(x, y, nullptr, n, k, s, g_ws, 512);
-                }});
-  vs.push_back({"ahead wave-records U4", true, [=](hipStream_t s) {
-                  return mavg_wave::launch_ahead_wave<float, double, 1, 4, 4, 1, 2, false, 1, 0>(x, y, nullptr, n, k, s, g_ws, 512);
-                }});
-  AH(8, 1, 512, 2, 1)
-  AH(2, 1, 1024, 2, 1)
-#define AHR(U, W)                                                                                       \
-  vs.push_back({"ahead rc U" #U " w" #W, true, [=](hipStream_t s) {                                       \
-                  return launch_ahead_scan<float, double, 1, 4, U, 1, 2, true, W>(x, y, nullptr, n, k, s, g_ws, 512); \
-                }});
-  AHR(4, 1)
-  AHR(8, 1)
-#define OP(U, NT)                                                                                       \
-  vs.push_back({"onepass U" #U " NT" #NT, true, [=](hipStream_t s) {                                      \
-                  return launch_onepass_scan<float, double, 1, 4, U, NT>(x, y, nullptr, n, k, s, g_ws);        \
-                }});
-  OP(1, 0)
-  OP(2, 0)
-  OP(4, 0)
-  OP(2, 1)
-  OP(2, 8)
-  OP(4, 8)
+  AH2(4, false, false, 1024, false, 1) AH2(4, false, false, 1024, false, 9) AH2(4, false, false, 512, false, 9)
+  AH2(4, true, true, 512, true, 1) AH2(4, true, true, 512, true, 9) AH2(4, true, true, 1024, true, 9)
+  AH2(4, false, true, 512, true, 9) AH2(4, false, true, 1024, true, 9) AH2(4, true, true, 768, true, 9)
 #define TILES(U, NT, WG)                                                                                \
   vs.push_back({"tileS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                               \
-                  return launch_tile_scan<float, double, 1, 4, U, false, NT, WG, true>(x, y, nullptr, n, k, s, 64); \
+                  return launch_tile_scan<float, double, 1, 4, U, false, NT, WG, true>(Sig{x, y, nullptr, n}, k, s, 64); \
                 }});
   TILES(2, 0, 256)
   TILES(2, 1, 256)
@@ -376,12 +338,6 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   TILES(2, 1, 1024)
   TILES(2, 5, 1024)
   TILES(2, 13, 1024)
-#define LBN(U, NT)                                                                                      \
-  vs.push_back({"lookbackN U" #U " nt" #NT, true, [=](hipStream_t s) {                                     \
-                  return launch_lookback_scan<float, double, 1, 4, U, NT>(x, y, nullptr, n, k, s, g_ws);       \
-                }});
-  LBN(2, 0)
-  LBN(2, 1)
   TILE(1, 0, 64)
   TILE(2, 0, 64)
   TILE(2, 1, 64)
@@ -395,7 +351,7 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
                   ScanTuning t;
                   t.xcd_remap = 1;
                   t.seg_chunks = std::max(4, 4 * ((k - 1 + 2047) / 2048));
-                  return launch_scan<float, double, 1, 4, 2, false, 2, 0>(x, y, nullptr, n, k, s, t);
+                  return launch_scan<float, double, 1, 4, 2, false, 2, 0>(Sig{x, y, nullptr, n}, k, s, t);
                 }});
   vs.push_back({"f32 product mavg_run", true, [=](hipStream_t s) {
                   return mavg_run(x, y, n, 1, k, MAVG_F32, MAVG_ALGO_AUTO, 0, nullptr, g_ws.ptr, g_ws.bytes, s);
@@ -426,15 +382,15 @@ template <>
 void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_t* y, long long n, int k) {
 #define ITILE(U, M)                                                                                       \
   vs.push_back({"i16 tile U" #U " remap" #M, true, [=](hipStream_t s) {                                    \
-                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, 0>(x, y, nullptr, n, k, s, M); \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, 0>(Sig{x, y, nullptr, n}, k, s, M); \
                 }});
 #define ITILENT(U, NT)                                                                                    \
   vs.push_back({"i16 tile U" #U " NT" #NT, true, [=](hipStream_t s) {                                      \
-                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT>(x, y, nullptr, n, k, s, 1); \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT>(Sig{x, y, nullptr, n}, k, s, 1); \
                 }});
 #define ITILENTR(U, NT, M)                                                                                \
   vs.push_back({"i16 tile U" #U " NT" #NT " remap" #M, true, [=](hipStream_t s) {                          \
-                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT>(x, y, nullptr, n, k, s, M); \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT>(Sig{x, y, nullptr, n}, k, s, M); \
                 }});
 #define IPROD()                                                                                           \
   vs.push_back({"i16 product mavg_run", true, [=](hipStream_t s) {                                        \
@@ -442,70 +398,37 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                 }});
 #define IDIRECT(U)                                                                                        \
   vs.push_back({"i16 direct U" #U, true, [=](hipStream_t s) {                                              \
-                  return launch_direct<int16_t, int32_t, 1, 8, U>(x, y, nullptr, n, k, s, 1);               \
+                  return launch_direct<int16_t, int32_t, 1, 8, U>(Sig{x, y, nullptr, n}, k, s, 1);               \
                 }});
 #define STILE(U, NT, M)                                                                                   \
   vs.push_back({"i16 stereo tile U" #U " NT" #NT " remap" #M, true, [=](hipStream_t s) {                   \
-                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT>(x, y, nullptr, n / 2, k, s, M); \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT>(Sig{x, y, nullptr, n / 2}, k, s, M); \
                 }});
   if (g_channels == 2) {
     vs.push_back({"i16 stereo product mavg_run", true, [=](hipStream_t s) {
                     return mavg_run(x, y, n, 2, k, MAVG_I16, MAVG_ALGO_AUTO, 0, nullptr, g_ws.ptr, g_ws.bytes, s);
                   }});
-#define SLB(U)                                                                                          \
-  vs.push_back({"i16 stereo lookback U" #U, true, [=](hipStream_t s) {                                    \
-                  return launch_lookback_scan<int16_t, int32_t, 2, 4, U, 0>(x, y, nullptr, n / 2, k, s, g_ws); \
+#define SAH2(U, RC, DMA, D, W, NT)                                                                      \
+  vs.push_back({"i16 stereo ahead U" #U " rc" #RC " dma" #DMA " D" #D " w" #W " nt" #NT, true, [=](hipStream_t s) {\
+                  return launch_ahead_scan<int16_t, int32_t, 2, 4, U, NT, RC, DMA, W>(Sig{x, y, nullptr, n / 2}, k, s, g_ws, D); \
                 }});
-    SLB(1)
-    SLB(2)
-    SLB(4)
-#define SAH(U, D, W, ORD)                                                                               \
-  vs.push_back({"i16 stereo ahead U" #U " D" #D " w" #W " o" #ORD, true, [=](hipStream_t s) {             \
-                  return launch_ahead_scan<int16_t, int32_t, 2, 4, U, 1, ORD, false, W>(x, y, nullptr, n / 2, k, s, g_ws, D); \
+    SAH2(4, false, true, 768, false, 9) SAH2(4, false, true, 1024, false, 9)
+#define SAHDV(D, W, DV)                                                                                 \
+  vs.push_back({"i16 stereo ahead D" #D " w" #W " div" #DV, true, [=](hipStream_t s) {                   \
+                  return launch_ahead_scan<int16_t, int32_t, 2, 4, 4, 9, false, true, W, DV>(Sig{x, y, nullptr, n / 2}, k, s, g_ws, D); \
                 }});
-    SAH(4, 512, 1, 2)
-    vs.push_back({"i16 stereo ahead rc pf1", true, [=](hipStream_t s) {
-                    return launch_ahead_scan<int16_t, int32_t, 2, 4, 4, 1, 2, true, 1, 1>(x, y, nullptr, n / 2, k, s, g_ws, 512);
-                  }});
-    vs.push_back({"i16 stereo ahead tile-records pf1", true, [=](hipStream_t s) {
-                    return launch_ahead_scan<int16_t, int32_t, 2, 4, 4, 1, 2, false, 1, 1>(x, y, nullptr, n / 2, k, s, g_ws, 512);
-                  }});
-    vs.push_back({"i16 stereo ahead tile-records pf4", true, [=](hipStream_t s) {
-                    return launch_ahead_scan<int16_t, int32_t, 2, 4, 4, 1, 2, false, 1, 4>(x, y, nullptr, n / 2, k, s, g_ws, 512);
-                  }});
-    vs.push_back({"i16 stereo ahead wave-records U4", true, [=](hipStream_t s) {
-                    return mavg_wave::launch_ahead_wave<int16_t, int32_t, 2, 4, 4, 1, 2, false, 1, 0>(x, y, nullptr, n / 2, k, s, g_ws, 512);
-                  }});
-    SAH(2, 1024, 1, 2)
-#define SAH64(U, D)                                                                                     \
-  vs.push_back({"i16 stereo ahead i64 U" #U " D" #D, true, [=](hipStream_t s) {                           \
-                  return launch_ahead_scan<int16_t, int64_t, 2, 4, U, 1, 2, false, 1>(x, y, nullptr, n / 2, k, s, g_ws, D); \
-                }});
+    SAHDV(768, false, 1) SAHDV(1024, false, 1) SAHDV(512, false, 1) SAHDV(512, true, 1)
     if (k > 65535) {
-      SAH64(4, 512)
-      SAH64(2, 1024)
-      SAH64(2, 512)
-      SAH64(1, 1024)
     }
-#define SAHR(U, W)                                                                                      \
-  vs.push_back({"i16 stereo ahead rc U" #U " w" #W, true, [=](hipStream_t s) {                            \
-                  return launch_ahead_scan<int16_t, int32_t, 2, 4, U, 1, 2, true, W>(x, y, nullptr, n / 2, k, s, g_ws, 512); \
-                }});
-    SAHR(4, 1)
-    SAHR(4, 6)
-    SAHR(2, 1)
-    SAHR(8, 1)
-#define SOP(U)                                                                                          \
-  vs.push_back({"i16 stereo onepass U" #U, true, [=](hipStream_t s) {                                     \
-                  return launch_onepass_scan<int16_t, int32_t, 2, 4, U, 0>(x, y, nullptr, n / 2, k, s, g_ws); \
-                }});
-    SOP(1)
-    SOP(2)
-    SOP(4)
 #define STILES(U, NT, WG)                                                                               \
   vs.push_back({"i16 stereo tileS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                   \
-                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, WG, false>(x, y, nullptr, n / 2, k, s, 64); \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, WG, false>(Sig{x, y, nullptr, n / 2}, k, s, 64); \
                 }});
+#define STILEDV(U, NT, DV)                                                                              \
+  vs.push_back({"i16 stereo tile U" #U " nt" #NT " div" #DV, true, [=](hipStream_t s) {                   \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, 256, false, DV>(Sig{x, y, nullptr, n / 2}, k, s, 64); \
+                }});
+    STILEDV(4, 3, 0) STILEDV(4, 3, 1) STILEDV(4, 13, 0) STILEDV(4, 13, 1)
     STILES(4, 0, 256)
     STILES(4, 3, 256)
     STILES(4, 4, 256)
@@ -519,7 +442,7 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
     STILES(2, 13, 1024)
 #define SHTS(U, NT, WG)                                                                                 \
   vs.push_back({"i16 stereo hillisS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                 \
-                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, true, NT, WG>(x, y, nullptr, n / 2, k, s); \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, true, NT, WG>(Sig{x, y, nullptr, n / 2}, k, s); \
                 }});
     SHTS(4, 0, 256)
     SHTS(4, 3, 256)
@@ -529,7 +452,7 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
     SHTS(4, 13, 512)
 #define STILEWG(U, WG, RC)                                                                              \
   vs.push_back({"i16 stereo tile U" #U " wg" #WG " rc" #RC, true, [=](hipStream_t s) {                    \
-                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, 0, WG, RC>(x, y, nullptr, n / 2, k, s, 64); \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, 0, WG, RC>(Sig{x, y, nullptr, n / 2}, k, s, 64); \
                 }});
     STILEWG(4, 256, false)
     STILEWG(2, 512, false)
@@ -539,7 +462,7 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
     STILEWG(4, 512, true)
 #define STILENR(U, NT)                                                                                  \
   vs.push_back({"i16 stereo tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                      \
-                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, 256, false>(x, y, nullptr, n / 2, k, s); \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, 256, false>(Sig{x, y, nullptr, n / 2}, k, s); \
                 }});
     STILENR(4, 3)
     STILENR(4, 0)
@@ -553,13 +476,13 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                     ScanTuning t;
                     t.xcd_remap = 1;
                     t.seg_chunks = std::max(4, 4 * ((k - 1 + 2047) / 2048));
-                    return launch_scan<int16_t, int32_t, 2, 4, 2, false, 2, 0>(x, y, nullptr, n / 2, k, s, t);
+                    return launch_scan<int16_t, int32_t, 2, 4, 2, false, 2, 0>(Sig{x, y, nullptr, n / 2}, k, s, t);
                   }});
     return;
   }
 #define ITILEWG(U, WG, RC)                                                                              \
   vs.push_back({"i16 tile U" #U " wg" #WG " rc" #RC, true, [=](hipStream_t s) {                           \
-                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, 0, WG, RC>(x, y, nullptr, n, k, s, 64); \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, 0, WG, RC>(Sig{x, y, nullptr, n}, k, s, 64); \
                 }});
   ITILEWG(8, 256, false)
   ITILEWG(4, 256, false)
@@ -568,66 +491,27 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   ITILEWG(4, 512, true)
   ITILEWG(2, 1024, false)
   ITILEWG(1, 1024, false)
-#define ILB(U)                                                                                          \
-  vs.push_back({"i16 lookback U" #U, true, [=](hipStream_t s) {                                           \
-                  return launch_lookback_scan<int16_t, int32_t, 1, 8, U, 0>(x, y, nullptr, n, k, s, g_ws);     \
+#define IAH2(U, RC, DMA, D, W, NT)                                                                      \
+  vs.push_back({"i16 ahead U" #U " rc" #RC " dma" #DMA " D" #D " w" #W " nt" #NT, true, [=](hipStream_t s) { \
+                  return launch_ahead_scan<int16_t, int32_t, 1, 8, U, NT, RC, DMA, W>(Sig{x, y, nullptr, n}, k, s, g_ws, D); \
                 }});
-  ILB(1)
-  ILB(2)
-  ILB(4)
-#define IAH(U, D, W, ORD)                                                                               \
-  vs.push_back({"i16 ahead U" #U " D" #D " w" #W " o" #ORD, true, [=](hipStream_t s) {                    \
-                  return launch_ahead_scan<int16_t, int32_t, 1, 8, U, 1, ORD, false, W>(x, y, nullptr, n, k, s, g_ws, D); \
+  IAH2(4, false, true, 512, true, 9) IAH2(4, false, true, 1024, false, 9)
+#define IAHDV(D, W, DV)                                                                                 \
+  vs.push_back({"i16 ahead D" #D " w" #W " div" #DV, true, [=](hipStream_t s) {                          \
+                  return launch_ahead_scan<int16_t, int32_t, 1, 8, 4, 9, false, true, W, DV>(Sig{x, y, nullptr, n}, k, s, g_ws, D); \
                 }});
-  IAH(4, 512, 1, 2)
-  vs.push_back({"i16 ahead rc pf4", true, [=](hipStream_t s) {
-                  return launch_ahead_scan<int16_t, int32_t, 1, 8, 4, 1, 2, true, 1, 4>(x, y, nullptr, n, k, s, g_ws, 512);
-                }});
-  vs.push_back({"i16 ahead tile-records pf1", true, [=](hipStream_t s) {
-                  return launch_ahead_scan<int16_t, int32_t, 1, 8, 4, 1, 2, false, 1, 1>(x, y, nullptr, n, k, s, g_ws, 512);
-                }});
-  vs.push_back({"i16 ahead tile-records pf4", true, [=](hipStream_t s) {
-                  return launch_ahead_scan<int16_t, int32_t, 1, 8, 4, 1, 2, false, 1, 4>(x, y, nullptr, n, k, s, g_ws, 512);
-                }});
-  vs.push_back({"i16 ahead wave-records U4", true, [=](hipStream_t s) {
-                  return mavg_wave::launch_ahead_wave<int16_t, int32_t, 1, 8, 4, 1, 2, false, 1, 0>(x, y, nullptr, n, k, s, g_ws, 512);
-                }});
-  IAH(2, 1024, 1, 2)
-#define IAH64(U, D)                                                                                     \
-  vs.push_back({"i16 ahead i64 U" #U " D" #D, true, [=](hipStream_t s) {                                  \
-                  return launch_ahead_scan<int16_t, int64_t, 1, 8, U, 1, 2, false, 1>(x, y, nullptr, n, k, s, g_ws, D); \
-                }});
+  IAHDV(512, true, 1) IAHDV(1024, false, 1) IAHDV(768, false, 1)
   if (k > 65535) {
-    IAH64(4, 512)
-    vs.push_back({"i16 ahead i64 U4 pf1", true, [=](hipStream_t s) {
-                    return launch_ahead_scan<int16_t, int64_t, 1, 8, 4, 1, 2, false, 1, 1>(x, y, nullptr, n, k, s, g_ws, 512);
-                  }});
-    vs.push_back({"i16 ahead i64 U4 pf4", true, [=](hipStream_t s) {
-                    return launch_ahead_scan<int16_t, int64_t, 1, 8, 4, 1, 2, false, 1, 4>(x, y, nullptr, n, k, s, g_ws, 512);
-                  }});
-    IAH64(2, 1024)
-    IAH64(2, 512)
-    IAH64(1, 1024)
   }
-#define IAHR(U, W)                                                                                      \
-  vs.push_back({"i16 ahead rc U" #U " w" #W, true, [=](hipStream_t s) {                                   \
-                  return launch_ahead_scan<int16_t, int32_t, 1, 8, U, 1, 2, true, W>(x, y, nullptr, n, k, s, g_ws, 512); \
-                }});
-  IAHR(4, 1)
-  IAHR(4, 6)
-  IAHR(2, 1)
-  IAHR(8, 1)
-#define IOP(U)                                                                                          \
-  vs.push_back({"i16 onepass U" #U, true, [=](hipStream_t s) {                                            \
-                  return launch_onepass_scan<int16_t, int32_t, 1, 8, U, 0>(x, y, nullptr, n, k, s, g_ws);      \
-                }});
-  IOP(1)
-  IOP(2)
-  IOP(4)
 #define ITILES(U, NT, WG)                                                                               \
   vs.push_back({"i16 tileS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                          \
-                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, WG, false>(x, y, nullptr, n, k, s, 64); \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, WG, false>(Sig{x, y, nullptr, n}, k, s, 64); \
                 }});
+#define ITILEDV(U, NT, DV)                                                                              \
+  vs.push_back({"i16 tile U" #U " nt" #NT " div" #DV, true, [=](hipStream_t s) {                          \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, 256, false, DV>(Sig{x, y, nullptr, n}, k, s, 64); \
+                }});
+  ITILEDV(4, 3, 0) ITILEDV(4, 3, 1)
   ITILES(4, 0, 256)
   ITILES(4, 3, 256)
   ITILES(4, 4, 256)
@@ -641,7 +525,7 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   ITILES(2, 13, 1024)
 #define IHTS(U, NT, WG)                                                                                 \
   vs.push_back({"i16 hillisS U" #U " nt" #NT " wg" #WG, true, [=](hipStream_t s) {                        \
-                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, true, NT, WG>(x, y, nullptr, n, k, s); \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, true, NT, WG>(Sig{x, y, nullptr, n}, k, s); \
                 }});
   IHTS(4, 0, 256)
   IHTS(4, 3, 256)
@@ -651,7 +535,7 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   IHTS(4, 13, 512)
 #define ITILENR(U, NT)                                                                                  \
   vs.push_back({"i16 tile U" #U " NT" #NT " noRC", true, [=](hipStream_t s) {                             \
-                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, 256, false>(x, y, nullptr, n, k, s); \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, 256, false>(Sig{x, y, nullptr, n}, k, s); \
                 }});
   ITILENR(4, 3)
   ITILENR(8, 0)
@@ -665,7 +549,7 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                   ScanTuning t;
                   t.xcd_remap = 1;
                   t.seg_chunks = std::max(4, 4 * ((k - 1 + 4095) / 4096));
-                  return launch_scan<int16_t, int32_t, 1, 8, 2, false, 2, 0>(x, y, nullptr, n, k, s, t);
+                  return launch_scan<int16_t, int32_t, 1, 8, 2, false, 2, 0>(Sig{x, y, nullptr, n}, k, s, t);
                 }});
   IPROD()
   if (k <= 64) {
