@@ -267,6 +267,15 @@ __device__ __forceinline__ long long remap_tile(unsigned b, unsigned nb, int mod
   return (long long)(((i >> g) << (g + 3)) + (x << g) + (i & ((1u << g) - 1u)));
 }
 
+// One 16-B LDS-DMA load per lane (global_load_lds_dwordx4): lane l's 16 bytes
+// land at lds_wave + 16 l; lds_wave must be wave-uniform (it goes to M0).
+// NT: non-temporal (aux = 2).
+template <bool NT = false>
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave, 16, 0, NT ? 2 : 0);
+}
+
 // non-temporal (streamed-once) policy bits of the NT template parameters
 constexpr int kNtStore = 1;
 constexpr int kNtLoad = 2;

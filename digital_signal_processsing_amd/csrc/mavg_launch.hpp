@@ -147,7 +147,7 @@ int launch_scan(const Sig& sg, int k, hipStream_t st, ScanTuning tune = ScanTuni
 // 0.763 of peak, mono equal; the look-ahead scan measured the other way,
 // tools/tune/tune_scan.hip "div" variants)
 template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, int WG = kWG,
-          bool RC = true, int DV = (sizeof(T) == 2 ? 1 : 0)>
+          bool RC = true, int DV = (sizeof(T) == 2 ? 1 : 0), bool DMA = false>
 int launch_tile_scan(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
   constexpr int TF = WG * F * U;
   constexpr int NSEG = U * (WG / 64);
@@ -172,9 +172,9 @@ int launch_tile_scan(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
   if (p.ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dv=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
-             "remap=%d",
-             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC, DV,
+             "tile_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dv=%d,dma=%d> grid=%lld block=%d lds=%zu "
+             "tile_frames=%d remap=%d",
+             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC, DV, (int)DMA,
              p.ntiles, WG, lds, TF, xcd_remap);
     return MAVG_OK;
   }
@@ -182,12 +182,12 @@ int launch_tile_scan(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
     static std::once_flag once;
     static hipError_t attr = hipSuccess;
     std::call_once(once, [] {
-      attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_scan_kernel<T, A, C, F, U, HS, NT, WG, RC, DV>),
+      attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_scan_kernel<T, A, C, F, U, HS, NT, WG, RC, DV, DMA>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_budget(WG));
     });
     if (attr != hipSuccess) return MAVG_ERR_HIP;
   }
-  hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, WG, RC, DV>), dim3((unsigned)p.ntiles), dim3(WG), lds, st,
+  hipLaunchKernelGGL((tile_scan_kernel<T, A, C, F, U, HS, NT, WG, RC, DV, DMA>), dim3((unsigned)p.ntiles), dim3(WG), lds, st,
                      p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
@@ -374,6 +374,17 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
       if (fits(2, 1024))
         return launch_tile_scan<T, A, C, F, 2, false, kNtS, 1024, false>(sg, k, st);
     } else {
+      // fp32 mono (round 2): the halo and the tile staged by LDS-DMA, 512-thread
+      // workgroups (2^30 samples, fraction of peak, in-process A/B against the
+      // round-1 rules: k=64 0.825 vs 0.802, k=256 0.819 vs 0.795, k=1024 0.810
+      // vs 0.801, k=2048 0.801 vs 0.794, k=4096 0.788 vs 0.778;
+      // profiles/r02_tuning/r02_tdma*)
+      constexpr bool kD = true;
+      constexpr int kDV = 0;
+      if (C == 1 && halo_bytes <= 8192 && fits(2, 512))
+        return launch_tile_scan<T, A, C, F, 2, false, kNtS, 512, true, kDV, kD>(sg, k, st);
+      if (C == 1 && halo_bytes <= 16384 && fits(4, 512))
+        return launch_tile_scan<T, A, C, F, 4, false, kNtS, 512, true, kDV, kD>(sg, k, st);
       if (C == 1 && halo_bytes <= 512 && fits(2, kWG))
         return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, true>(sg, k, st);
       if (halo_bytes <= 4096 && fits(2, kWG))

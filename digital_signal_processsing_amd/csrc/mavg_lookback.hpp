@@ -194,15 +194,6 @@ struct AheadParams {
   OutParams o;
 };
 
-// One 16-B LDS-DMA load per lane (global_load_lds_dwordx4): lane l's 16 bytes
-// land at lds_wave + 16 l; lds_wave must be wave-uniform (it goes to M0).
-// NT: non-temporal (aux = 2).
-template <bool NT = false>
-__device__ __forceinline__ void glds16(const void* g, void* lds_wave) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)lds_wave, 16, 0, NT ? 2 : 0);
-}
-
 // wave_record (mavg_lookback.hpp) with one unit in registers at a time: the
 // same additions in the same order, so the same bits.  For the rare paths.
 template <typename T, typename SA, int C, int F, int U, int WG>

@@ -47,8 +47,11 @@ struct TileParams {
 //     barrier and rebuild the in-lane prefix afterwards from the LDS stage
 //     (the tile and x[n-k] are both staged), in the same order, so the
 //     outputs are bitwise the same with U*F*C fewer live accumulators.
+// DMA (Blelloch flavour, 16-B units): interior tiles stage the halo and the
+//     tile in LDS by LDS-DMA (global_load_lds_dwordx4, no staging registers,
+//     no ds_write) and the scan reads x from the stage.
 template <typename T, typename A, int C, int F, int U, bool HS, int NT = kNtLoad | kNtStore, int WG = kWG,
-          bool RC = true, int DV = 0>
+          bool RC = true, int DV = 0, bool DMA = false>
 __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
@@ -84,10 +87,41 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   const long long h0 = t0 - Ha;              // first staged halo frame
   const bool tile_full = (t0 + TF <= nframes);
 
-  // ---- tile -> registers -> LDS ----
+  constexpr bool kDma = DMA && !HS && IO::kVec && VE * (int)sizeof(T) == 16;
+  const bool dma = kDma && tile_full && h0 >= 0 && !eio;  // uniform
+  constexpr bool kXs = kRC || kDma;  // x read back from the stage
+  // ---- tile -> registers -> LDS (or straight to LDS by LDS-DMA) ----
   U_t x[U];
+  if constexpr (kDma) {
+    if (dma) {
+      const int wq = __builtin_amdgcn_readfirstlane(w);
+      unsigned char* sb = reinterpret_cast<unsigned char*>(stage);
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < U; ++u) {
+        const long long f = t0 + (long long)(u * WG + tid) * F;
+        unsigned char* d = sb + (Hu + u * WG + wq * 64) * 16;
+        if constexpr ((NT & kNtSplit) != 0) {
+          // frames the next tile's halo re-reads keep the default policy (L2)
+          if ((u * WG + tid) * F + F > TF - Ha) glds16<false>(in + f * C, d);
+          else glds16<true>(in + f * C, d);
+        } else {
+          glds16<(NT & kNtLoad) != 0>(in + f * C, d);
+        }
+      }
+      for (int j0 = 0; j0 < Hu; j0 += WG) {
+        const int j = j0 + tid;
+        if (j < Hu) glds16<(NT & kNtHalo) != 0>(in + (h0 + (long long)j * F) * C, sb + (j0 + wq * 64) * 16);
+      }
+      if (tid == 0) {
+        U_t z;
+#pragma unroll
+        for (int i = 0; i < VE; ++i) z.e[i] = (T)0;
+        IO::store(stage + (Hu + U * WG) * VE, z);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U && !dma; ++u) {
     const long long f = t0 + (long long)(u * WG + tid) * F;
     if (tile_full) {
       if constexpr ((NT & kNtSplit) != 0) {
@@ -105,7 +139,7 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
     }
   }
   // ---- halo -> LDS (re-read of the previous tile's tail: L2) ----
-  {
+  if (!dma) {
     const bool halo_fast = h0 >= 0;
     for (int j = tid; j < Hu; j += WG) {
       const long long f = h0 + (long long)j * F;
@@ -121,13 +155,15 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
       IO::store(stage + j * VE, h);
     }
   }
+  if (!dma) {
 #pragma unroll
-  for (int u = 0; u < U; ++u) IO::store(stage + (Hu + u * WG + tid) * VE, x[u]);
-  if (tid == 0) {
-    U_t z;
+    for (int u = 0; u < U; ++u) IO::store(stage + (Hu + u * WG + tid) * VE, x[u]);
+    if (tid == 0) {
+      U_t z;
 #pragma unroll
-    for (int i = 0; i < VE; ++i) z.e[i] = (T)0;
-    IO::store(stage + (Hu + U * WG) * VE, z);   // pad unit (k < F reads one unit past the tile)
+      for (int i = 0; i < VE; ++i) z.e[i] = (T)0;
+      IO::store(stage + (Hu + U * WG) * VE, z);   // pad unit (k < F reads one unit past the tile)
+    }
   }
   __syncthreads();
 
@@ -206,11 +242,14 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
 #pragma unroll
           for (int c = 0; c < C; ++c) run[c] += to_acc<A>(xu.e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
       } else {
+        U_t xu;
+        if constexpr (kXs) xu = IO::load(stage + (Hu + j) * VE);
+        else xu = x[u];
 #pragma unroll
         for (int fr = 0; fr < F; ++fr)
 #pragma unroll
           for (int c = 0; c < C; ++c) {
-            const A d = to_acc<A>(x[u].e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
+            const A d = to_acc<A>(xu.e[fr * C + c]) - to_acc<A>(xk.e[fr * C + c]);
             v[u][fr][c] = fr == 0 ? d : v[u][fr - 1][c] + d;
           }
 #pragma unroll

@@ -101,11 +101,14 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
 def test_plan_describes_launch_without_gpu():
     import digital_signal_processsing_amd as dsp
     p = dsp.plan(1 << 30, 1024)
-    assert p.startswith("tile_scan<f32,acc=f64,C=1,F=4,U=2,blelloch") and "grid=524288" in p, p
+    # fp32 mono: 512-thread tiles staged by LDS-DMA up to 16 KiB of halo
+    assert p.startswith("tile_scan<f32,acc=f64,C=1,F=4,U=2,blelloch") and "grid=262144" in p, p
+    assert "block=512" in p and "dma=1" in p, p
     # split cache policy (nt tile loads but the halo tail, nt halo, nt stores)
-    assert "nt=13" in p and "nt=13" in dsp.plan(1 << 30, 4096), p
-    assert "nt=3" in dsp.plan(1 << 30, 64)  # tiny halo: everything non-temporal
+    assert "nt=13" in p and "nt=13" in dsp.plan(1 << 30, 4096) and "nt=13" in dsp.plan(1 << 30, 64), p
     assert "U=4" in dsp.plan(1 << 30, 4096) and "block=512" in dsp.plan(1 << 30, 4096)
+    # stereo fp32 keeps the register-staged tile
+    assert "dma=0" in dsp.plan(1 << 30, 1024, channels=2)
     assert dsp.plan(1 << 20, 70_000).startswith("ahead_scan<f32")
     assert dsp.plan(1 << 20, 70_000, algo="hillis").startswith("segment_scan<") and "xkg=1" in dsp.plan(
         1 << 20, 70_000, algo="hillis")

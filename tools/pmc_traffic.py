@@ -51,7 +51,7 @@ def plan_key(plan):
     wg = re.search(r"block=(\d+)", plan).group(1)
     if fam == "tile_scan":
         args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["nt"], wg, "true" if kv.get("rc", "1") == "1" else "false",
-                kv.get("dv", "0"))
+                kv.get("dv", "0"), "true" if kv.get("dma", "0") == "1" else "false")
     elif fam == "direct":
         args = (T, acc, kv["C"], kv["F"], kv["U"], wg)
     elif fam == "ahead_scan":

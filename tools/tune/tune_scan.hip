@@ -273,6 +273,13 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   TILENR(2, 0)
   TILENR(4, 3)
   TILENR(8, 0)
+#define TDMA(U, NT, WG, DMA)                                                                            \
+  vs.push_back({"tdma U" #U " nt" #NT " wg" #WG " dma" #DMA, true, [=](hipStream_t s) {                   \
+                  return launch_tile_scan<float, double, 1, 4, U, false, NT, WG, true, 0, DMA>(Sig{x, y, nullptr, n}, k, s, 64); \
+                }});
+  TDMA(2, 13, 256, false) TDMA(2, 13, 256, true) TDMA(2, 3, 256, false) TDMA(2, 3, 512, false) TDMA(2, 3, 512, true)
+  TDMA(4, 13, 512, false) TDMA(4, 13, 512, true) TDMA(2, 13, 512, false) TDMA(2, 13, 512, true) TDMA(1, 13, 1024, true)
+  TDMA(2, 13, 1024, true)
 #define TILEWG(U, WG)                                                                                   \
   vs.push_back({"tile U" #U " wg" #WG " rc", true, [=](hipStream_t s) {                                   \
                   return launch_tile_scan<float, double, 1, 4, U, false, 0, WG>(Sig{x, y, nullptr, n}, k, s, 64); \
@@ -429,6 +436,11 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                   return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, 256, false, DV>(Sig{x, y, nullptr, n / 2}, k, s, 64); \
                 }});
     STILEDV(4, 3, 0) STILEDV(4, 3, 1) STILEDV(4, 13, 0) STILEDV(4, 13, 1)
+#define STDMA(U, NT, DMA)                                                                               \
+  vs.push_back({"i16 stereo tdma U" #U " nt" #NT " dma" #DMA, true, [=](hipStream_t s) {                  \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, 256, false, 1, DMA>(Sig{x, y, nullptr, n / 2}, k, s, 64); \
+                }});
+    STDMA(4, 3, false) STDMA(4, 3, true) STDMA(8, 13, false) STDMA(8, 13, true) STDMA(8, 12, true) STDMA(8, 9, true)
     STILES(4, 0, 256)
     STILES(4, 3, 256)
     STILES(4, 4, 256)
@@ -512,6 +524,11 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                   return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, 256, false, DV>(Sig{x, y, nullptr, n}, k, s, 64); \
                 }});
   ITILEDV(4, 3, 0) ITILEDV(4, 3, 1)
+#define ITDMA(U, NT, DMA)                                                                               \
+  vs.push_back({"i16 tdma U" #U " nt" #NT " dma" #DMA, true, [=](hipStream_t s) {                         \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, 256, false, 1, DMA>(Sig{x, y, nullptr, n}, k, s, 64); \
+                }});
+  ITDMA(4, 3, false) ITDMA(4, 3, true) ITDMA(8, 13, false) ITDMA(8, 13, true) ITDMA(4, 13, true)
   ITILES(4, 0, 256)
   ITILES(4, 3, 256)
   ITILES(4, 4, 256)
