@@ -377,6 +377,11 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   TILEM(8, 16)
   TILEM(8, 64)
   TILEM(8, 256)
+#define DIRW(U, WG)                                                                                     \
+  vs.push_back({"dirw U" #U " wg" #WG, true, [=](hipStream_t s) {                                         \
+                  return launch_direct<float, double, 1, 4, U, WG>(Sig{x, y, nullptr, n}, k, s, 64);         \
+                }});
+  DIRW(1, 256) DIRW(2, 256) DIRW(4, 256) DIRW(1, 512) DIRW(2, 512) DIRW(1, 1024)
   DIRECTM(1)
   DIRECTM(16)
   DIRECTM(64)
@@ -440,7 +445,12 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   vs.push_back({"i16 stereo tdma U" #U " nt" #NT " dma" #DMA, true, [=](hipStream_t s) {                  \
                   return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, 256, false, 1, DMA>(Sig{x, y, nullptr, n / 2}, k, s, 64); \
                 }});
-    STDMA(4, 3, false) STDMA(4, 3, true) STDMA(8, 13, false) STDMA(8, 13, true) STDMA(8, 12, true) STDMA(8, 9, true)
+    STDMA(4, 3, false) STDMA(4, 3, true) STDMA(8, 13, false) STDMA(8, 13, true)
+#define STDMW(U, NT, WG, DMA)                                                                           \
+  vs.push_back({"i16 stereo tdmw U" #U " nt" #NT " wg" #WG " dma" #DMA, true, [=](hipStream_t s) {        \
+                  return launch_tile_scan<int16_t, int32_t, 2, 4, U, false, NT, WG, false, 1, DMA>(Sig{x, y, nullptr, n / 2}, k, s, 64); \
+                }});
+    STDMW(2, 3, 256, false) STDMW(2, 3, 512, false) STDMW(2, 3, 512, true) STDMW(2, 13, 512, true) STDMW(4, 13, 512, true) STDMW(4, 3, 512, false)
     STILES(4, 0, 256)
     STILES(4, 3, 256)
     STILES(4, 4, 256)
@@ -529,6 +539,11 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                   return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, 256, false, 1, DMA>(Sig{x, y, nullptr, n}, k, s, 64); \
                 }});
   ITDMA(4, 3, false) ITDMA(4, 3, true) ITDMA(8, 13, false) ITDMA(8, 13, true) ITDMA(4, 13, true)
+#define ITDMW(U, NT, WG, DMA)                                                                           \
+  vs.push_back({"i16 tdmw U" #U " nt" #NT " wg" #WG " dma" #DMA, true, [=](hipStream_t s) {               \
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, U, false, NT, WG, false, 1, DMA>(Sig{x, y, nullptr, n}, k, s, 64); \
+                }});
+  ITDMW(2, 3, 256, false) ITDMW(2, 3, 512, false) ITDMW(2, 3, 512, true) ITDMW(2, 13, 512, true) ITDMW(4, 13, 512, true) ITDMW(4, 3, 512, false)
   ITILES(4, 0, 256)
   ITILES(4, 3, 256)
   ITILES(4, 4, 256)
