@@ -162,6 +162,25 @@ struct UnitIO {
     }
     return u;
   }
+  // The two aligned LDS units an extraction (below) reads from.  Volatile
+  // keeps each a whole 16-B load: an extraction at o >= 1 never reads a.e[0]
+  // (nor b.e[VE-1]), and with plain loads the compiler narrows the pair into a
+  // misaligned ds_read_b96 + ds_read_u16, which bank-conflict (int16 mono at
+  // k = 1023 or 1020: 12 conflict cycles per wave, 0.725 of peak against 0.81
+  // at k = 1024; profiles/r02_tuning/r02_odd, pmc_odd).  An empty asm that
+  // pins the registers instead forces a wait after every load (0.68).
+  __device__ __forceinline__ static Unit<T, VE> load_whole(const T* p) {  // LDS only
+    Unit<T, VE> u;
+    if constexpr (kVec) {
+      using R = typename RawVec<kBytes>::type;
+      const R r = *(const volatile __attribute__((address_space(3))) R*)p;  // p points into LDS
+      __builtin_memcpy(&u, &r, kBytes);
+    } else {
+#pragma unroll
+      for (int i = 0; i < VE; ++i) u.e[i] = p[i];
+    }
+    return u;
+  }
   // Global-memory forms.  eio (uniform): the pointer is only element-aligned
   // (a frame-unit launch on a misaligned view, mavg_api.hip), so a
   // multi-element unit moves as element accesses instead of one vector access.

@@ -363,13 +363,18 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
     // Longer halos take bigger workgroups: the LDS stage per workgroup then
     // carries more waves (tools/tune/sweep_wg.sh, sweep_wg2.sh).
     if constexpr (sizeof(T) == 2) {
-      // round 2, LDS-DMA staging (in-process A/B at k=1024, 2^30 samples,
-      // profiles/r02_tuning/r02_g, r02_tdma*): mono U2 x 512 threads 0.820 vs
-      // 0.800; stereo U8 x 256 0.826 vs 0.812 (0.815 vs 0.791 on another box)
+      // round 2, LDS-DMA staging where x[n-k] is unit-aligned (k*C a multiple
+      // of the lane unit; in-process A/B, 2^30 samples, bursts of 10 launches,
+      // profiles/r02_tuning/r02_g, r02_i16sw3, r02_odd3): mono U2 x 512 threads
+      // 0.811-0.820 vs 0.800-0.803 at k = 16..2048; stereo U8 x 256 0.807-0.826
+      // vs 0.780-0.822 at k = 768..1024 (U4 wins below).  With a misaligned
+      // x[n-k] the DMA tile reads x back from LDS beside two units for x[n-k]
+      // and measured 0.785 against 0.80 for the register-staged U4 tile.
       constexpr int kDV = 1;
-      if (C == 1 && halo_bytes <= 4096 && fits(2, 512))
+      const bool xk_aligned = ((long long)k * C) % VE == 0;
+      if (C == 1 && xk_aligned && halo_bytes <= 4096 && fits(2, 512))
         return launch_tile_scan<T, A, C, F, 2, false, kNtS, 512, false, kDV, true>(sg, k, st);
-      if (C == 2 && halo_bytes > 256 && halo_bytes <= 4096 && fits(8, kWG))
+      if (C == 2 && xk_aligned && halo_bytes > 2048 && halo_bytes <= 4096 && fits(8, kWG))
         return launch_tile_scan<T, A, C, F, 8, false, kNtS, kWG, false, kDV, true>(sg, k, st);
       if (halo_bytes <= 256 && fits(2, kWG))
         return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, false>(sg, k, st);

@@ -411,8 +411,8 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
         xk = IO::load(stage + e);
       } else {
         const int e_lo = e - p.xk_off;
-        U_t a0 = IO::load(stage + e_lo);
-        U_t a1 = IO::load(stage + e_lo + VE);
+        U_t a0 = IO::load_whole(stage + e_lo);
+        U_t a1 = IO::load_whole(stage + e_lo + VE);
         xk = extract(a0, a1, p.xk_off);
       }
     } else {

@@ -148,8 +148,8 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
           // x[n-k] straddles two aligned units: read both, shift by xk_off elements
           const int e_lo = qk * C - p.xk_off;              // aligned unit holding the first element
           const int e_hi = (e_lo + VE == R * C) ? 0 : e_lo + VE;
-          U_t a = IO::load(ring + e_lo);
-          U_t b = IO::load(ring + e_hi);
+          U_t a = IO::load_whole(ring + e_lo);
+          U_t b = IO::load_whole(ring + e_hi);
           xk = extract(a, b, p.xk_off);
         }
       } else {

@@ -192,8 +192,8 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
         xk = IO::load(stage + e);
       } else {
         const int e_lo = e - p.xk_off;
-        U_t a = IO::load(stage + e_lo);
-        U_t b = IO::load(stage + e_lo + VE);
+        U_t a = IO::load_whole(stage + e_lo);
+        U_t b = IO::load_whole(stage + e_lo + VE);
         xk = extract(a, b, p.xk_off);
       }
     } else {

@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""A/B two builds of libmavg.so inside bench.py's environment (torch-allocated
+buffers, one launch per HIP-event pair on torch's current stream, launches
+back to back): the in-process tuner and bench.py disagreed on a tile rule,
+and this separates the kernel from the harness.
+
+    python tools/tune/ab_libs.py LIB_A LIB_B [--k 1024] [--c 1] [--dtype i16] [--rounds 6] [--steps 20]
+
+Prints, per library, the mean / median of the per-launch times over all
+rounds (rounds alternate A, B, A, B ...) and the same-stream copy for scale.
+"""
+import argparse
+import ctypes
+import statistics
+
+import torch
+
+import digital_signal_processsing_amd as dsp
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs=2)
+    ap.add_argument("--k", type=int, default=1024)
+    ap.add_argument("--c", type=int, default=1)
+    ap.add_argument("--dtype", default="i16", choices=["i16", "f32"])
+    ap.add_argument("--log2n", type=int, default=30)
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=20)
+    a = ap.parse_args()
+    n = 1 << a.log2n
+    tdt = torch.int16 if a.dtype == "i16" else torch.float32
+    code = dsp.I16 if a.dtype == "i16" else dsp.F32
+    x = dsp.fill_synthetic(n, tdt, seed=0x5EED, device="cuda")
+    y = torch.empty_like(x)
+    libs = []
+    for p in a.libs:
+        lib = ctypes.CDLL(p)
+        lib.mavg_run.restype = ctypes.c_int
+        lib.mavg_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_size_t, ctypes.c_void_p]
+        buf = ctypes.create_string_buffer(512)
+        lib.mavg_plan.restype = ctypes.c_int
+        lib.mavg_plan(ctypes.c_size_t(n), a.c, a.k, code, 0, 0, buf, ctypes.c_size_t(512))
+        libs.append((p, lib, buf.value.decode()))
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def launch(lib):
+        st = lib.mavg_run(x.data_ptr(), y.data_ptr(), n, a.c, a.k, code, 0, 0, None, None, 0, stream)
+        assert st == 0, st
+
+    def copy():
+        y.copy_(x)
+
+    times = {p: [] for p, _, _ in libs}
+    times["torch copy_"] = []
+    for p, lib, _ in libs:  # warm-up
+        for _ in range(5):
+            launch(lib)
+    torch.cuda.synchronize()
+    outs = []
+    for r in range(a.rounds):
+        order = libs if r % 2 == 0 else libs[::-1]
+        for p, lib, _ in order:
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+            for e0, e1 in ev:
+                e0.record()
+                launch(lib)
+                e1.record()
+            torch.cuda.synchronize()
+            times[p] += [e0.elapsed_time(e1) for e0, e1 in ev]
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+        for e0, e1 in ev:
+            e0.record()
+            copy()
+            e1.record()
+        torch.cuda.synchronize()
+        times["torch copy_"] += [e0.elapsed_time(e1) for e0, e1 in ev]
+    for p, lib, _ in libs:
+        launch(lib)
+        torch.cuda.synchronize()
+        outs.append(y.clone())
+    byt = 2 * x.element_size() * n
+    print(f"n=2^{a.log2n} k={a.k} C={a.c} dtype={a.dtype} rounds={a.rounds} steps={a.steps}  outputs equal: "
+          f"{bool(torch.equal(outs[0], outs[1]))}")
+    for p, lib, plan in libs + [("torch copy_", None, "")]:
+        t = times[p]
+        mean, med = statistics.mean(t), statistics.median(t)
+        print(f"{p:48s} mean {mean:.4f} ms ({byt / mean / 1e6 / 8000:.4f} of 8 TB/s)  median {med:.4f} "
+              f"({byt / med / 1e6 / 8000:.4f})  min {min(t):.4f}  {plan}")
+
+
+if __name__ == "__main__":
+    main()

@@ -179,8 +179,12 @@ int run(int lg, int k, int rounds) {
   }
   for (auto& v : vs) { v.launch(st); v.launch(st); }
   CK(hipStreamSynchronize(st));
+  // the start of each round rotates, so every variant follows every other one
+  // equally often (a fixed order measured the variant right after the copy
+  // 1-3 % slow)
   for (int r = 0; r < rounds; ++r) {
-    for (auto& v : vs) {
+    for (size_t j = 0; j < vs.size(); ++j) {
+      auto& v = vs[(j + r) % vs.size()];
       CK(hipEventRecord(e0, st));
       for (int b = 0; b < g_burst; ++b) v.launch(st);
       CK(hipEventRecord(e1, st));
@@ -363,6 +367,9 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   vs.push_back({"f32 product mavg_run", true, [=](hipStream_t s) {
                   return mavg_run(x, y, n, 1, k, MAVG_F32, MAVG_ALGO_AUTO, 0, nullptr, g_ws.ptr, g_ws.bytes, s);
                 }});
+  vs.push_back({"f32 disp", true, [=](hipStream_t s) {
+                  return dispatch_scan_f<float, double, 1, 4, false>(Sig{x, y, nullptr, n}, k, 0, s, g_ws);
+                }});
   TILEM(1, 1)
   TILEM(1, 64)
   TILEM(4, 1)
@@ -407,6 +414,9 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
 #define IPROD()                                                                                           \
   vs.push_back({"i16 product mavg_run", true, [=](hipStream_t s) {                                        \
                   return mavg_run(x, y, n, 1, k, MAVG_I16, MAVG_ALGO_AUTO, 0, nullptr, g_ws.ptr, g_ws.bytes, s); \
+                }});                                                                                                       \
+  vs.push_back({"i16 disp", true, [=](hipStream_t s) {                                                    \
+                  return dispatch_scan_f<int16_t, int32_t, 1, 8, false>(Sig{x, y, nullptr, n}, k, 0, s, g_ws);   \
                 }});
 #define IDIRECT(U)                                                                                        \
   vs.push_back({"i16 direct U" #U, true, [=](hipStream_t s) {                                              \
@@ -419,6 +429,11 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   if (g_channels == 2) {
     vs.push_back({"i16 stereo product mavg_run", true, [=](hipStream_t s) {
                     return mavg_run(x, y, n, 2, k, MAVG_I16, MAVG_ALGO_AUTO, 0, nullptr, g_ws.ptr, g_ws.bytes, s);
+                  }});
+    // the product's dispatch compiled into this binary (separates the library's
+    // code object and the C ABI's host path from the kernel itself)
+    vs.push_back({"i16 stereo disp", true, [=](hipStream_t s) {
+                    return dispatch_scan_f<int16_t, int32_t, 2, 4, false>(Sig{x, y, nullptr, n / 2}, k, 0, s, g_ws);
                   }});
 #define SAH2(U, RC, DMA, D, W, NT)                                                                      \
   vs.push_back({"i16 stereo ahead U" #U " rc" #RC " dma" #DMA " D" #D " w" #W " nt" #NT, true, [=](hipStream_t s) {\
