@@ -363,19 +363,10 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
     // Longer halos take bigger workgroups: the LDS stage per workgroup then
     // carries more waves (tools/tune/sweep_wg.sh, sweep_wg2.sh).
     if constexpr (sizeof(T) == 2) {
-      // round 2, LDS-DMA staging where x[n-k] is unit-aligned (k*C a multiple
-      // of the lane unit; in-process A/B, 2^30 samples, bursts of 10 launches,
-      // profiles/r02_tuning/r02_g, r02_i16sw3, r02_odd3): mono U2 x 512 threads
-      // 0.811-0.820 vs 0.800-0.803 at k = 16..2048; stereo U8 x 256 0.807-0.826
-      // vs 0.780-0.822 at k = 768..1024 (U4 wins below).  With a misaligned
-      // x[n-k] the DMA tile reads x back from LDS beside two units for x[n-k]
-      // and measured 0.785 against 0.80 for the register-staged U4 tile.
-      constexpr int kDV = 1;
-      const bool xk_aligned = ((long long)k * C) % VE == 0;
-      if (C == 1 && xk_aligned && halo_bytes <= 4096 && fits(2, 512))
-        return launch_tile_scan<T, A, C, F, 2, false, kNtS, 512, false, kDV, true>(sg, k, st);
-      if (C == 2 && xk_aligned && halo_bytes > 2048 && halo_bytes <= 4096 && fits(8, kWG))
-        return launch_tile_scan<T, A, C, F, 8, false, kNtS, kWG, false, kDV, true>(sg, k, st);
+      // int16 keeps register staging: LDS-DMA tiles won the in-process tuner's
+      // A/B (mono U2 x 512 0.811-0.820 vs 0.800-0.803) but lost 2-3.5 % in
+      // bench.py's own timing, one HIP-event pair per back-to-back launch
+      // (tools/tune/ab_libs.py, profiles/r02_tuning/r02_ablibs*); stereo tied
       if (halo_bytes <= 256 && fits(2, kWG))
         return launch_tile_scan<T, A, C, F, 2, false, kNt, kWG, false>(sg, k, st);
       if (halo_bytes <= 4096 && fits(4, kWG))
@@ -391,7 +382,9 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
       // workgroups (2^30 samples, fraction of peak, in-process A/B against the
       // round-1 rules: k=64 0.825 vs 0.802, k=256 0.819 vs 0.795, k=1024 0.810
       // vs 0.801, k=2048 0.801 vs 0.794, k=4096 0.788 vs 0.778;
-      // profiles/r02_tuning/r02_tdma*)
+      // profiles/r02_tuning/r02_tdma*); confirmed in bench.py's timing
+      // (tools/tune/ab_libs.py, r02_ablibs2): k=64 0.814 vs 0.780, k=1024 0.802
+      // vs 0.797, k=4096 0.781 vs 0.773 against the same tiles register-staged
       constexpr bool kD = true;
       constexpr int kDV = 0;
       if (C == 1 && halo_bytes <= 8192 && fits(2, 512))

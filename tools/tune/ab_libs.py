@@ -11,9 +11,13 @@ rounds (rounds alternate A, B, A, B ...) and the same-stream copy for scale.
 """
 import argparse
 import ctypes
+import os
 import statistics
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import digital_signal_processsing_amd as dsp
 
@@ -27,14 +31,20 @@ def main():
     ap.add_argument("--log2n", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--ypad", type=int, default=0, help="offset y by this many bytes inside a bigger buffer")
+    ap.add_argument("--blocks", type=int, nargs=2, default=[0, 0],
+                    help="block_size per library (0: the tuned dispatch; else the reference's block size)")
     a = ap.parse_args()
     n = 1 << a.log2n
     tdt = torch.int16 if a.dtype == "i16" else torch.float32
     code = dsp.I16 if a.dtype == "i16" else dsp.F32
     x = dsp.fill_synthetic(n, tdt, seed=0x5EED, device="cuda")
-    y = torch.empty_like(x)
+    pad = a.ypad // x.element_size()
+    ybuf = torch.empty(n + pad, dtype=tdt, device="cuda")
+    y = ybuf[pad:]
     libs = []
-    for p in a.libs:
+    blocks = {}
+    for li, p in enumerate(a.libs):
         lib = ctypes.CDLL(p)
         lib.mavg_run.restype = ctypes.c_int
         lib.mavg_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
@@ -42,12 +52,14 @@ def main():
                                  ctypes.c_size_t, ctypes.c_void_p]
         buf = ctypes.create_string_buffer(512)
         lib.mavg_plan.restype = ctypes.c_int
-        lib.mavg_plan(ctypes.c_size_t(n), a.c, a.k, code, 0, 0, buf, ctypes.c_size_t(512))
+        lib.mavg_plan(ctypes.c_size_t(n), a.c, a.k, code, 0, a.blocks[li], buf, ctypes.c_size_t(512))
+        p = f"{p} block={a.blocks[li]}"
         libs.append((p, lib, buf.value.decode()))
+        blocks[p] = a.blocks[li]
     stream = torch.cuda.current_stream().cuda_stream
 
-    def launch(lib):
-        st = lib.mavg_run(x.data_ptr(), y.data_ptr(), n, a.c, a.k, code, 0, 0, None, None, 0, stream)
+    def launch(lib, p):
+        st = lib.mavg_run(x.data_ptr(), y.data_ptr(), n, a.c, a.k, code, 0, blocks[p], None, None, 0, stream)
         assert st == 0, st
 
     def copy():
@@ -57,7 +69,7 @@ def main():
     times["torch copy_"] = []
     for p, lib, _ in libs:  # warm-up
         for _ in range(5):
-            launch(lib)
+            launch(lib, p)
     torch.cuda.synchronize()
     outs = []
     for r in range(a.rounds):
@@ -66,7 +78,7 @@ def main():
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
             for e0, e1 in ev:
                 e0.record()
-                launch(lib)
+                launch(lib, p)
                 e1.record()
             torch.cuda.synchronize()
             times[p] += [e0.elapsed_time(e1) for e0, e1 in ev]
@@ -78,11 +90,12 @@ def main():
         torch.cuda.synchronize()
         times["torch copy_"] += [e0.elapsed_time(e1) for e0, e1 in ev]
     for p, lib, _ in libs:
-        launch(lib)
+        launch(lib, p)
         torch.cuda.synchronize()
         outs.append(y.clone())
     byt = 2 * x.element_size() * n
-    print(f"n=2^{a.log2n} k={a.k} C={a.c} dtype={a.dtype} rounds={a.rounds} steps={a.steps}  outputs equal: "
+    print(f"n=2^{a.log2n} k={a.k} C={a.c} dtype={a.dtype} rounds={a.rounds} steps={a.steps} "
+          f"y-x={y.data_ptr() - x.data_ptr():#x}  outputs equal: "
           f"{bool(torch.equal(outs[0], outs[1]))}")
     for p, lib, plan in libs + [("torch copy_", None, "")]:
         t = times[p]

@@ -5,6 +5,8 @@
 //
 // build: make -C tools/tune
 // run:   tools/tune/tune_scan [log2n] [k] [rounds] [f32|i16] [burst] [filter] [channels (i16: 1|2)]
+//        burst > 0: launches per event pair (mean); burst < 0: -burst back-to-back launches with one
+//        event pair each, as bench.py times them (the two orderings can rank tile shapes differently)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -112,7 +114,8 @@ int run(int lg, int k, int rounds) {
   hipLaunchKernelGGL(synth_kernel<T>, dim3(4096), dim3(256), 0, st, x, n, (uint64_t)0x5EED, 0);
   CK(hipStreamSynchronize(st));
   int cus = device_cu_count();
-  printf("device CUs=%d n=2^%d k=%d rounds=%d dtype=%s\n", cus, lg, k, rounds, ES == 4 ? "f32" : "i16");
+  printf("device CUs=%d n=2^%d k=%d rounds=%d dtype=%s y-x=%#llx\n", cus, lg, k, rounds, ES == 4 ? "f32" : "i16",
+         (unsigned long long)((const char*)y - (const char*)x));
 
   std::vector<Variant> vs;
   const long long n4 = n * ES / 16;
@@ -136,6 +139,8 @@ int run(int lg, int k, int rounds) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  std::vector<hipEvent_t> ce(g_burst < 0 ? 2 * (-g_burst) : 0);
+  for (auto& e : ce) CK(hipEventCreate(&e));
   // reference output + correctness of every scan variant
   bool have_ref = false;
   {  // drop variants the launcher refuses (e.g. LDS over budget for this k)
@@ -185,6 +190,21 @@ int run(int lg, int k, int rounds) {
   for (int r = 0; r < rounds; ++r) {
     for (size_t j = 0; j < vs.size(); ++j) {
       auto& v = vs[(j + r) % vs.size()];
+      if (g_burst < 0) {
+        // bench.py's timing: -burst back-to-back launches, one event pair each
+        for (int b = 0; b < -g_burst; ++b) {
+          CK(hipEventRecord(ce[2 * b], st));
+          v.launch(st);
+          CK(hipEventRecord(ce[2 * b + 1], st));
+        }
+        CK(hipEventSynchronize(ce[2 * (-g_burst) - 1]));
+        for (int b = 0; b < -g_burst; ++b) {
+          float ms;
+          CK(hipEventElapsedTime(&ms, ce[2 * b], ce[2 * b + 1]));
+          v.ms.push_back(ms);
+        }
+        continue;
+      }
       CK(hipEventRecord(e0, st));
       for (int b = 0; b < g_burst; ++b) v.launch(st);
       CK(hipEventRecord(e1, st));
@@ -194,13 +214,20 @@ int run(int lg, int k, int rounds) {
       v.ms.push_back(ms / g_burst);
     }
   }
-  printf("%-28s %9s %9s %9s %9s %s\n", "variant", "med_ms", "min_ms", "GB/s", "frac8T", "mismatch");
+  // frac8T from the median; bench.py reports the mean (mfrac8T), which a
+  // variant with a few slow launches loses (int16 LDS-DMA tiles did)
+  printf("%-28s %9s %9s %9s %9s %s %9s\n", "variant", "med_ms", "min_ms", "GB/s", "frac8T", "mismatch", "mfrac8T");
   for (auto& v : vs) {
     std::vector<float> m = v.ms;
     std::sort(m.begin(), m.end());
     const float med = m[m.size() / 2], mn = m[0];
+    double mean = 0;
+    for (float t : m) mean += t;
+    mean /= (double)m.size();
     const double gbs = 2.0 * ES * n / (med * 1e-3) / 1e9;
-    printf("%-28s %9.4f %9.4f %9.1f %9.4f %llu\n", v.name.c_str(), med, mn, gbs, gbs / 8000.0, v.mism);
+    const double mgbs = 2.0 * ES * n / (mean * 1e-3) / 1e9;
+    printf("%-28s %9.4f %9.4f %9.1f %9.4f %llu %9.4f\n", v.name.c_str(), med, mn, gbs, gbs / 8000.0, v.mism,
+           mgbs / 8000.0);
   }
   CK(hipFree(x));
   CK(hipFree(y));
