@@ -24,6 +24,7 @@ CONFIGS = [
     ("hillis_2p30_k1024", 1 << 30, 1024, 1, "f32", "hillis"),
     ("i16_2p30_k1024", 1 << 30, 1024, 1, "i16", "blelloch"),
     ("i16_stereo_2p30_k44100", 1 << 30, 44100, 2, "i16", "blelloch"),  # 1 s windows on 44.1 kHz stereo PCM
+    ("i16_mono_2p30_k44100", 1 << 30, 44100, 1, "i16", "blelloch"),  # look-ahead scan, int16 mono
 ]
 
 
