@@ -63,7 +63,9 @@ __device__ __forceinline__ void pick_prefix_rt(int off, const A (&pc)[2 * F][C],
   }
 }
 
-template <typename T, typename A, int C, int F, int U, int WG = kWG>
+// NT: non-temporal policy bits (mavg_device.hpp): kNtLoad the tile's loads,
+// kNtHalo the halo's, kNtStore the output stores
+template <typename T, typename A, int C, int F, int U, int WG = kWG, int NT = 0>
 __global__ __launch_bounds__(WG) void direct_kernel(DirectParams p) {
   constexpr int VE = F * C;
   constexpr int TF = WG * F * U;
@@ -92,7 +94,7 @@ __global__ __launch_bounds__(WG) void direct_kernel(DirectParams p) {
   for (int u = 0; u < U; ++u) {
     const long long f = t0 + (long long)(u * WG + tid) * F;
     if (tile_full) {
-      xr[u] = IO::gload(in + f * C, eio);
+      xr[u] = IO::template gload<(NT & kNtLoad) != 0>(in + f * C, eio);
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(WG) void direct_kernel(DirectParams p) {
     const long long f = h0 + (long long)j * F;
     U_t h;
     if (halo_fast) {
-      h = IO::gload(in + f * C, eio);
+      h = IO::template gload<(NT & kNtHalo) != 0>(in + f * C, eio);
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(WG) void direct_kernel(DirectParams p) {
 #pragma unroll
       for (int c = 0; c < C; ++c) y.e[fr * C + c] = to_out<T, A>(wsum[fr][c], p.o);
     if (tile_full) {
-      IO::gstore(out + f * C, y, eio);
+      IO::template gstore<(NT & kNtStore) != 0>(out + f * C, y, eio);
     } else {
 #pragma unroll
       for (int fr = 0; fr < F; ++fr)

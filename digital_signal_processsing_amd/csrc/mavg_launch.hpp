@@ -450,7 +450,7 @@ int dispatch_scan(int C, bool vec, bool hs, const Sig& sg, int k, int block, hip
 }
 
 // ---- direct LDS-tiled launch ---------------------------------------------------
-template <typename T, typename A, int C, int F, int U = 1, int WG = kWG>
+template <typename T, typename A, int C, int F, int U = 1, int WG = kWG, int NT = 0>
 int launch_direct(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
   constexpr int TF = WG * F * U;
   constexpr int VE = F * C;
@@ -472,22 +472,29 @@ int launch_direct(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGr
   const long long nblk = (nframes + TF - 1) / TF;
   if (nblk > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
-    snprintf(g_plan->text, sizeof(g_plan->text), "direct<%s,acc=%s,C=%d,F=%d,U=%d> grid=%lld block=%d lds=%zu",
-             type_name<T>(), type_name<A>(), C, F, U, nblk, WG, lds);
+    snprintf(g_plan->text, sizeof(g_plan->text), "direct<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d> grid=%lld block=%d lds=%zu",
+             type_name<T>(), type_name<A>(), C, F, U, NT, nblk, WG, lds);
     return MAVG_OK;
   }
-  hipLaunchKernelGGL((direct_kernel<T, A, C, F, U, WG>), dim3((unsigned)nblk), dim3(WG), lds, st, p);
+  hipLaunchKernelGGL((direct_kernel<T, A, C, F, U, WG, NT>), dim3((unsigned)nblk), dim3(WG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
+// The tuned direct launch: two units per lane, non-temporal tile, halo and
+// output (2^28 fp32, k=7, in-process A/B, tools/tune/tune_scan.hip "dirnt":
+// 0.835 of peak vs 0.814 for one unit per lane with the default policy;
+// profiles/r02_tuning/r02_direct_nt/).  A reference block size keeps one unit
+// per lane in a workgroup of that size.
+constexpr int kNtDirect = kNtLoad | kNtHalo | kNtStore;
 template <typename T, typename A, int C, int F>
 int launch_direct_block(const Sig& sg, int k, int block, hipStream_t st) {
-  switch (block == 0 ? kWG : block_wg(block)) {
-    case 64: return launch_direct<T, A, C, F, 1, 64>(sg, k, st);
-    case 128: return launch_direct<T, A, C, F, 1, 128>(sg, k, st);
-    case 512: return launch_direct<T, A, C, F, 1, 512>(sg, k, st);
-    case 1024: return launch_direct<T, A, C, F, 1, 1024>(sg, k, st);
-    default: return launch_direct<T, A, C, F, 1, kWG>(sg, k, st);
+  switch (block == 0 ? 0 : block_wg(block)) {
+    case 0: return launch_direct<T, A, C, F, 2, kWG, kNtDirect>(sg, k, st);
+    case 64: return launch_direct<T, A, C, F, 1, 64, kNtDirect>(sg, k, st);
+    case 128: return launch_direct<T, A, C, F, 1, 128, kNtDirect>(sg, k, st);
+    case 512: return launch_direct<T, A, C, F, 1, 512, kNtDirect>(sg, k, st);
+    case 1024: return launch_direct<T, A, C, F, 1, 1024, kNtDirect>(sg, k, st);
+    default: return launch_direct<T, A, C, F, 1, kWG, kNtDirect>(sg, k, st);
   }
 }
 

@@ -53,7 +53,7 @@ def plan_key(plan):
         args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["nt"], wg, "true" if kv.get("rc", "1") == "1" else "false",
                 kv.get("dv", "0"), "true" if kv.get("dma", "0") == "1" else "false")
     elif fam == "direct":
-        args = (T, acc, kv["C"], kv["F"], kv["U"], wg)
+        args = (T, acc, kv["C"], kv["F"], kv["U"], wg, kv.get("nt", "0"))
     elif fam == "ahead_scan":
         b = {"0": "false", "1": "true"}
         args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], b[kv["rc"]], b[kv["dma"]], b[kv["wrec"]], kv["dv"])

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--c", type=int, default=1)
     ap.add_argument("--dtype", default="i16", choices=["i16", "f32"])
     ap.add_argument("--log2n", type=int, default=30)
+    ap.add_argument("--algo", type=int, default=0, help="mavg_algo (0 auto, 5 direct)")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--ypad", type=int, default=0, help="offset y by this many bytes inside a bigger buffer")
@@ -59,7 +60,7 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     def launch(lib, p):
-        st = lib.mavg_run(x.data_ptr(), y.data_ptr(), n, a.c, a.k, code, 0, blocks[p], None, None, 0, stream)
+        st = lib.mavg_run(x.data_ptr(), y.data_ptr(), n, a.c, a.k, code, a.algo, blocks[p], None, None, 0, stream)
         assert st == 0, st
 
     def copy():

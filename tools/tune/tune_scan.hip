@@ -416,6 +416,12 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
                   return launch_direct<float, double, 1, 4, U, WG>(Sig{x, y, nullptr, n}, k, s, 64);         \
                 }});
   DIRW(1, 256) DIRW(2, 256) DIRW(4, 256) DIRW(1, 512) DIRW(2, 512) DIRW(1, 1024)
+#define DIRNT(U, WG, NT)                                                                                \
+  vs.push_back({"dirnt U" #U " wg" #WG " nt" #NT, true, [=](hipStream_t s) {                              \
+                  return launch_direct<float, double, 1, 4, U, WG, NT>(Sig{x, y, nullptr, n}, k, s, kRemapGroup); \
+                }});
+  DIRNT(1, 256, 0) DIRNT(1, 256, 1) DIRNT(1, 256, 3) DIRNT(1, 256, 9) DIRNT(1, 256, 11)
+  DIRNT(2, 256, 1) DIRNT(2, 256, 11) DIRNT(1, 512, 1) DIRNT(1, 512, 11)
   DIRECTM(1)
   DIRECTM(16)
   DIRECTM(64)
