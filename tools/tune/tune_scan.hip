@@ -310,7 +310,7 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
                 }});
   TDMA(2, 13, 256, false) TDMA(2, 13, 256, true) TDMA(2, 3, 256, false) TDMA(2, 3, 512, false) TDMA(2, 3, 512, true)
   TDMA(4, 13, 512, false) TDMA(4, 13, 512, true) TDMA(2, 13, 512, false) TDMA(2, 13, 512, true) TDMA(1, 13, 1024, true)
-  TDMA(2, 13, 1024, true)
+  TDMA(2, 13, 1024, true) TDMA(3, 13, 1024, true) TDMA(3, 13, 512, true)
 #define TILEWG(U, WG)                                                                                   \
   vs.push_back({"tile U" #U " wg" #WG " rc", true, [=](hipStream_t s) {                                   \
                   return launch_tile_scan<float, double, 1, 4, U, false, 0, WG>(Sig{x, y, nullptr, n}, k, s, 64); \
