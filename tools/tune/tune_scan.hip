@@ -571,6 +571,12 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                   return launch_ahead_scan<int16_t, int32_t, 1, 8, 4, 9, false, true, W, DV>(Sig{x, y, nullptr, n}, k, s, g_ws, D); \
                 }});
   IAHDV(512, true, 1) IAHDV(1024, false, 1) IAHDV(768, false, 1)
+  // 8-B units (F=4): x[n-k] unit-aligned when k = 4 mod 8 (e.g. 44100), register-staged
+#define IAH4(U, D, W, DV)                                                                               \
+  vs.push_back({"i16 ahead8B U" #U " D" #D " w" #W " div" #DV, true, [=](hipStream_t s) {                  \
+                  return launch_ahead_scan<int16_t, int32_t, 1, 4, U, 9, false, false, W, DV>(Sig{x, y, nullptr, n}, k, s, g_ws, D); \
+                }});
+  IAH4(8, 512, true, 0) IAH4(8, 1024, false, 0) IAH4(4, 512, true, 0) IAH4(8, 512, true, 1)
   if (k > 65535) {
   }
 #define ITILES(U, NT, WG)                                                                               \
