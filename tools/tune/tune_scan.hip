@@ -577,6 +577,15 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
                   return launch_ahead_scan<int16_t, int32_t, 1, 4, U, 9, false, false, W, DV>(Sig{x, y, nullptr, n}, k, s, g_ws, D); \
                 }});
   IAH4(8, 512, true, 0) IAH4(8, 1024, false, 0) IAH4(4, 512, true, 0) IAH4(8, 512, true, 1)
+  // tiny windows: AUTO's tile shape (halo <= 256 B: U2 nt3 x 256, magic division) vs the direct kernel
+  vs.push_back({"i16 autotile U2 nt3", true, [=](hipStream_t s) {
+                  return launch_tile_scan<int16_t, int32_t, 1, 8, 2, false, 3, 256, false>(Sig{x, y, nullptr, n}, k, s);
+                }});
+#define IDIRNT(U, NT)                                                                                   \
+  vs.push_back({"i16 dirnt U" #U " nt" #NT, true, [=](hipStream_t s) {                                    \
+                  return launch_direct<int16_t, int32_t, 1, 8, U, 256, NT>(Sig{x, y, nullptr, n}, k, s, kRemapGroup); \
+                }});
+  IDIRNT(2, 11) IDIRNT(1, 11) IDIRNT(1, 0)
   if (k > 65535) {
   }
 #define ITILES(U, NT, WG)                                                                               \
