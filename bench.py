@@ -298,6 +298,44 @@ def check_output(y, n, k, C, dt, seed, rank, samples=64, span=4096):
     return {"slices": len(starts), "span_frames": span, "mismatches": bad}
 
 
+def shard_timing(args, x, y, k, C, algo, ev, hev, value, n, rank, world):
+    """N > 1: what the sharded step costs each rank beyond one plain launch.
+    Per rank, from the timed steps' events on the launch stream: the halo wait
+    (interior end -> head start: the stream waits for the RCCL receive) and the
+    head launch.  Then, in the same run, each rank times K whole-shard launches
+    with no halo (the N=1 step on its own shard, wall clock between barriers),
+    so the weak-scaling efficiency comes out of this one run:
+        weak_scaling_efficiency = value / (N * mean per-rank single-launch rate)."""
+    import torch
+    import torch.distributed as dist
+    import digital_signal_processsing_amd as dsp
+    halo_ms = statistics.mean(b.elapsed_time(h[0]) for (_, b), h in zip(ev, hev))
+    head_ms = statistics.mean(h[0].elapsed_time(h[1]) for h in hev)
+    for _ in range(max(1, args.warmup)):
+        dsp.moving_average_into(x, y, k, C, algo)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dsp.moving_average_into(x, y, k, C, algo)
+    torch.cuda.synchronize()
+    single_s = time.perf_counter() - t0
+    rate = n * args.steps / single_s / 1e9
+    mine = {"rank": rank, "halo_wait_ms": round(halo_ms, 4), "head_ms": round(head_ms, 4),
+            "single_launch_gsamples_s": round(rate, 3)}
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    mean_rate = statistics.mean(r["single_launch_gsamples_s"] for r in every)
+    return {
+        "weak_scaling_efficiency": round(value / (world * mean_rate), 4),
+        "single_launch_gsamples_s_mean": round(mean_rate, 3),
+        "per_rank": every,
+        "method": "per rank: K whole-shard launches without halo in this run (wall clock between a barrier and "
+                  "a synchronize); halo_wait = interior end -> head start on the launch stream; efficiency = "
+                  "value / (N x mean single-launch rate)",
+    }
+
+
 def run_workload(args, name, rank, world, with_cpu):
     import torch
     import digital_signal_processsing_amd as dsp
@@ -324,12 +362,15 @@ def run_workload(args, name, rank, world, with_cpu):
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
+    hev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)] if world > 1 else None
 
     def step(i=None, j=0):
         if world > 1:
             # halo send/recv posted first, interior launch overlaps it, head launch after it
             sharded_moving_average(x, k, C, algo, out=y, recv_buf=hist_buf[: (k - 1) * C],
-                                   events=ev[i] if i is not None else None)
+                                   events=ev[i] if i is not None else None,
+                                   head_events=hev[i] if i is not None else None)
             return
         if i is not None:
             j = i % rot
@@ -403,6 +444,8 @@ def run_workload(args, name, rank, world, with_cpu):
                       "the head launch are outside it and only in value / ms_per_step"),
         },
     }
+    if world > 1:
+        line["scaling_detail"] = shard_timing(args, x, y, k, C, algo, ev, hev, value, n, rank, world)
     if args.check:
         res = check_output(y, n, k, C, dt, seed, rank)
         if world > 1:

@@ -159,7 +159,11 @@ def moving_average(x, grade: int, channels: int = 1, algo="auto", history=None,
         with torch.cuda.stream(stream):
             out = torch.empty_like(x)
         moving_average_into(x, out, grade, channels, algo, history, block_size, stream)
+        # the kernel reads x and history on `stream`: keep the caching
+        # allocator from handing their blocks out again before it ends
         x.record_stream(stream)
+        if history is not None:
+            history.record_stream(stream)
         return out
     out = torch.empty_like(x)
     moving_average_into(x, out, grade, channels, algo, history, block_size, stream)

@@ -195,16 +195,22 @@ void profile_mode(const Options& o, int C, size_t n, const std::vector<int16_t>&
 int run_gpu(const Options& o, int C, const std::vector<int16_t>& samples, std::vector<int16_t>& out) {
   CsvLogger logger(o.csv);
   const size_t n = samples.size() / (size_t)C * (size_t)C;  // whole frames
-  if (kV.banner) {
+  if (kV.banner) {  // the variant's own header (hillis_steele_averager.cu:205-207, profilable_*.cu)
     std::cout << kV.banner << std::endl;
-    std::cout << "Samples: " << samples.size() << std::endl;
-    std::cout << "point: " << o.grade << std::endl;
-    std::cout << "block Size: " << o.block << std::endl;
+    if (kV.algo == MAVG_ALGO_HILLIS_SCALAR) {
+      std::cout << "total samples: " << samples.size() << std::endl;
+      std::cout << "point: " << o.grade << std::endl;
+    } else {
+      std::cout << "Samples: " << samples.size() << std::endl;
+      std::cout << "point: " << o.grade << std::endl;
+      std::cout << "block Size: " << o.block << std::endl;
+    }
   }
-  {  // the launch the block size maps to (workgroup = the next power of two >= 64, see mavg.h)
+  {  // the launch the block size maps to (workgroup = the next power of two >= 64,
+     // see mavg.h): on stderr, so stdout stays the reference's report
     char plan[512] = {0};
     if (n > 0) MAVG_CHECK(mavg_plan(n, C, o.grade, MAVG_I16, kV.algo, o.block, plan, sizeof(plan)));
-    std::cout << "Kernel: " << plan << std::endl;
+    std::cerr << "Kernel: " << plan << std::endl;
   }
   if (o.standard) {
     std::cout << "\n--- MEM MODE: STANDARD (Discrete) ---" << std::endl;

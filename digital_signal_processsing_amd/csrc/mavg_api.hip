@@ -214,12 +214,26 @@ int mavg_run(const void* d_in, void* d_out, size_t n_samples, int channels, int 
   if (ai != ao || ai % fb != 0)
     return launch_algo(sf, dtype, C, frame_sig(d_in, d_out, d_history, nframes, 0), grade, block_size, s, ws);
   const long long p = std::min<long long>(nframes, (long long)(((size_t)vu - ai) / fb));
-  st = launch_algo(sf, dtype, C, frame_sig(d_in, d_out, d_history, p, 0), grade, block_size, s, ws);
-  if (st != MAVG_OK || p == nframes) return st;
+  const Sig head = frame_sig(d_in, d_out, d_history, p, 0);
   const size_t off = (size_t)p * fb;
   const void* hist_body = d_history != nullptr ? static_cast<const char*>(d_history) + off : nullptr;
   const Sig body{static_cast<const char*>(d_in) + off, static_cast<char*>(d_out) + off, hist_body, nframes - p,
                  (int)p, 0};
+  // both launches are first made in plan mode: an error of the second one
+  // (e.g. a workspace that covers the head but not the body) must leave
+  // nothing on the stream (mavg.h)
+  for (int part = 0; part < (p == nframes ? 1 : 2); ++part) {
+    LaunchPlan plan{};
+    g_plan = &plan;
+    st = part == 0 ? launch_algo(sf, dtype, C, head, grade, block_size, nullptr, ws)
+                   : launch_algo(algo, dtype, C, body, grade, block_size, nullptr, ws);
+    g_plan = nullptr;
+    if (st != MAVG_OK) return st;
+    if (plan.ws_bytes > 0 && (d_ws == nullptr || ws_bytes < plan.ws_bytes)) return MAVG_ERR_WORKSPACE;
+    if (plan.ws_bytes > 0 && !aligned(d_ws, 16)) return MAVG_ERR_MISALIGNED;
+  }
+  st = launch_algo(sf, dtype, C, head, grade, block_size, s, ws);
+  if (st != MAVG_OK || p == nframes) return st;
   return launch_algo(algo, dtype, C, body, grade, block_size, s, ws);
 }
 
@@ -246,8 +260,8 @@ int mavg_plan(size_t n_samples, int channels, int grade, int dtype, int algo, in
 int mavg_fill_synthetic(void* d_out, size_t n_samples, int dtype, uint64_t seed, uint64_t offset, int dist,
                         void* stream) {
   if (dtype != MAVG_I16 && dtype != MAVG_F32) return MAVG_ERR_INVALID_ARG;
-  if (dist != 0 && dist != 1) return MAVG_ERR_INVALID_ARG;
-  if (dist == 1 && dtype != MAVG_F32) return MAVG_ERR_INVALID_ARG;
+  if (dist < 0 || dist > 2) return MAVG_ERR_INVALID_ARG;
+  if (dist != 0 && dtype != MAVG_F32) return MAVG_ERR_INVALID_ARG;
   if (n_samples == 0) return MAVG_OK;
   if (d_out == nullptr) return MAVG_ERR_INVALID_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -9,7 +9,6 @@ std::atomic<int> g_test_ahead_slots{-1};
 std::atomic<int> g_test_ahead_spin{-1};
 
 // ---- per-device attribute cache (no stream work, capture-safe) --------------
-constexpr int kMaxDevices = 64;
 static std::atomic<int> g_cu_count[kMaxDevices];
 
 int device_cu_count() {

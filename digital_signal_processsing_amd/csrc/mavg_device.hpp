@@ -6,6 +6,23 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Debug build (make DEBUG=1 -> libmavg_debug.so): device bounds checks on LDS
+// stage indices, x[n-k] extractions, tile indices and record slots; a failed
+// check prints (what, block, thread, two values) and traps.  Compiled out of
+// the release library.
+#ifdef MAVG_DEBUG
+#define MAVG_DCHECK(cond, what, a, b)                                                                   \
+  do {                                                                                                \
+    if (!(cond)) {                                                                                    \
+      printf("mavg debug check failed: %s (block %u thread %u: %lld, %lld)\n", what, blockIdx.x,      \
+             threadIdx.x, (long long)(a), (long long)(b));                                            \
+      __builtin_trap();                                                                               \
+    }                                                                                                 \
+  } while (0)
+#else
+#define MAVG_DCHECK(cond, what, a, b) ((void)0)
+#endif
+
 namespace mavg {
 
 constexpr int kWG = 256;          // threads per workgroup (4 wave64s)

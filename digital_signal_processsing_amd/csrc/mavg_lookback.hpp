@@ -128,11 +128,17 @@ __device__ __forceinline__ uint32_t gran_word(double v, int h) {
   return h == 0 ? (uint32_t)__double2loint(v) : (uint32_t)__double2hiint(v);
 }
 __device__ __forceinline__ uint32_t gran_word(int32_t v, int) { return (uint32_t)v; }
+__device__ __forceinline__ uint32_t gran_word(int64_t v, int h) {
+  return h == 0 ? (uint32_t)(uint64_t)v : (uint32_t)((uint64_t)v >> 32);
+}
 template <typename SA> __device__ __forceinline__ SA gran_value(const uint32_t (&w)[GranCount<SA>::n]);
 template <> __device__ __forceinline__ double gran_value<double>(const uint32_t (&w)[2]) {
   return __hiloint2double((int)w[1], (int)w[0]);
 }
 template <> __device__ __forceinline__ int32_t gran_value<int32_t>(const uint32_t (&w)[1]) { return (int32_t)w[0]; }
+template <> __device__ __forceinline__ int64_t gran_value<int64_t>(const uint32_t (&w)[2]) {
+  return (int64_t)(((uint64_t)w[1] << 32) | w[0]);
+}
 
 // One wave's share of a tile's sum (wave slot wv): lane l sums its units
 // u*WG + wv*64 + l over u, frames and channels in order, then one DPP wave

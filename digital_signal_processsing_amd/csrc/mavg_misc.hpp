@@ -34,6 +34,20 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// dist 2 (oracle synth_f32_dist2): an Irwin-Hall integer from the four 14-bit
+// fields, times fl64(1/3000), times 2^-s (s from the 5 bits above), rounded to
+// fp32 -- each step one correctly rounded IEEE operation (no add, so nothing
+// to contract into an fma), so host and device agree bit for bit
+__device__ __forceinline__ float synth_f32_dist2(uint64_t h) {
+  const long long i = (long long)(h & 0x3fffu) + (long long)((h >> 14) & 0x3fffu) +
+                      (long long)((h >> 28) & 0x3fffu) + (long long)((h >> 42) & 0x3fffu) - 32766;
+  const int b = (int)((h >> 56) & 31u);
+  const int s = b < 8 ? 0 : b - 8;
+  const double p = __longlong_as_double((long long)(1023 - s) << 52);  // 2^-s, exactly
+  const double v = (double)i * (1.0 / 3000.0);
+  return (float)(v * p);
+}
+
 template <typename T>
 __global__ __launch_bounds__(kWG) void synth_kernel(T* __restrict__ out, long long n, uint64_t base, int dist) {
   const long long stride = (long long)gridDim.x * kWG;
@@ -42,7 +56,9 @@ __global__ __launch_bounds__(kWG) void synth_kernel(T* __restrict__ out, long lo
     if constexpr (sizeof(T) == 2) {
       out[i] = (T)(int16_t)(uint16_t)(h >> 48);
     } else {
-      out[i] = dist == 1 ? (float)(h >> 40) * (1.0f / 16777216.0f) : (float)(int16_t)(uint16_t)(h >> 48);
+      out[i] = dist == 1   ? (float)(h >> 40) * (1.0f / 16777216.0f)
+               : dist == 2 ? synth_f32_dist2(h)
+                           : (float)(int16_t)(uint16_t)(h >> 48);
     }
   }
 }

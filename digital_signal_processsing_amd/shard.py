@@ -98,12 +98,14 @@ def _peer(group_rank: int, group) -> int:
 
 
 def split_moving_average_into(x_local, out, grade: int, channels: int = 1, algo="auto", history=None,
-                              events=None, before_head=None) -> None:
+                              events=None, before_head=None, head_events=None) -> None:
     """out = moving average of x_local given `history` (the (grade-1)*channels
     samples before it, None = zeros) as two launches: the interior (frames >=
     head_frames(), history taken from inside x_local) first, then -- after
     `before_head()` (e.g. waiting for the halo) -- the head.  Same result as
-    one launch with `history`; the split only lets the halo arrive late."""
+    one launch with `history`; the split only lets the halo arrive late.
+    `events` / `head_events`: optional (start, end) CUDA events recorded around
+    the interior / the head launch (bench.py's per-rank timing)."""
     from . import moving_average_into
 
     C = channels
@@ -118,13 +120,17 @@ def split_moving_average_into(x_local, out, grade: int, channels: int = 1, algo=
             events[1].record()
     if before_head is not None:
         before_head()
+    if head_events is not None:
+        head_events[0].record()
     if head > 0:
         moving_average_into(x_local[: head * C], out[: head * C], grade, C, algo,
                             history=history() if callable(history) else history)
+    if head_events is not None:
+        head_events[1].record()
 
 
 def sharded_moving_average(x_local, grade: int, channels: int = 1, algo="auto", group=None,
-                           out=None, recv_buf=None, events=None):
+                           out=None, recv_buf=None, events=None, head_events=None):
     """Moving average of the global signal whose shard this rank holds
     (device tensor); returns this rank's shard of the output.  The halo
     send/recv is posted first and overlaps the interior launch; only the head
@@ -140,5 +146,6 @@ def sharded_moving_average(x_local, grade: int, channels: int = 1, algo="auto", 
         for r in reqs:
             r.wait()
 
-    split_moving_average_into(x_local, out, grade, channels, algo, history=hist, events=events, before_head=wait)
+    split_moving_average_into(x_local, out, grade, channels, algo, history=hist, events=events, before_head=wait,
+                              head_events=head_events)
     return out

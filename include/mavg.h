@@ -35,8 +35,11 @@
  * mavg_run never allocates, never synchronises, never exits, and only
  * enqueues work on `stream` (a hipStream_t; NULL = the legacy default
  * stream), so it can be captured into a HIP graph.  d_in is const (the
- * reference scans in place; this library does not).  Re-entrant, no globals
- * other than a per-device attribute cache.
+ * reference scans in place; this library does not).  Thread-safe and
+ * re-entrant; the only process state is per DEVICE (keyed on hipGetDevice):
+ * the CU count and, per kernel, whether its dynamic-LDS limit has been raised
+ * on that device -- so one process may drive several devices -- plus the
+ * process-wide test hook mavg_test_ahead_schedule.
  */
 #ifndef MAVG_H
 #define MAVG_H
@@ -123,7 +126,9 @@ int mavg_resolve_algo(size_t n_samples, int channels, int grade, int dtype, int 
 
 /* Counter-based synthetic signal on the device: x[i] for global index
  * offset+i, from splitmix64(seed + offset + i).  dist 0: int16-valued
- * (as int16 or as float); dist 1: uniform [0,1) floats (MAVG_F32 only). */
+ * (as int16 or as float); dist 1: uniform [0,1) floats; dist 2: zero-mean,
+ * mixed-scale, non-dyadic floats whose fp64 window sums round (the fp32
+ * rounding-stress input of the parity tests).  dist 1 and 2: MAVG_F32 only. */
 int mavg_fill_synthetic(void* d_out, size_t n_samples, int dtype, uint64_t seed,
                         uint64_t offset, int dist, void* stream);
 

@@ -53,6 +53,8 @@ def _load():
     lib.oracle_check_synth_f32.argtypes = [p, sz, i, i, u64, u64, i, ctypes.c_double, i, pu, pu, pd]
     lib.oracle_check_synth_f32.restype = ctypes.c_int
     lib.oracle_check_synth_i16.argtypes = [p, sz, i, i, u64, u64, i, pu, pu]
+    lib.oracle_check_synth_f32_exact.argtypes = [p, sz, i, i, u64, u64, i, ctypes.c_double, i, p, p]
+    lib.oracle_check_synth_f32_exact.restype = ctypes.c_int
     lib.oracle_check_synth_i16.restype = ctypes.c_int
     lib.oracle_synth_i16.restype = None
     lib.oracle_synth_f32.restype = None
@@ -150,9 +152,12 @@ def check_synth(y: np.ndarray, k: int, channels: int = 1, seed: int = 0x5EED, of
     bit-exact, fp32 within ``rtol`` relative.  Chunked over ``threads`` cores;
     exact for these inputs (see oracle_check_synth_f32 in mavg_oracle.c).
     Returns {"checked", "mismatches", "first_bad" (sample index or None),
-    "max_rel" (fp32)}."""
+    "max_rel" (fp32)}.  fp32 dist 2 (whose fp64 sums round) goes to
+    check_synth_exact."""
     threads = threads or min(16, len(os.sched_getaffinity(0)))
     y = np.ascontiguousarray(y)
+    if y.dtype == np.float32 and dist == 2:
+        return check_synth_exact(y, k, channels, seed, offset, dist, rtol, threads)
     bad, first = ctypes.c_uint64(0), ctypes.c_uint64(0)
     if y.dtype == np.int16:
         rc = _load().oracle_check_synth_i16(_ptr(y), y.size, channels, k, seed, offset, threads,
@@ -169,3 +174,45 @@ def check_synth(y: np.ndarray, k: int, channels: int = 1, seed: int = 0x5EED, of
         raise ValueError(f"oracle_check_synth: bad arguments (n={y.size}, C={channels}, k={k}, offset={offset})")
     return {"checked": int(y.size), "mismatches": int(bad.value),
             "first_bad": None if bad.value == 0 else int(first.value), "max_rel": worst}
+
+
+def check_synth_exact(y: np.ndarray, k: int, channels: int = 1, seed: int = 0x5EED, offset: int = 0,
+                      dist: int = 2, rtol: float = 1e-5, threads: int = 0) -> dict:
+    """fp32 check of EVERY sample against the EXACT window sum (__int128 fixed
+    point, oracle_check_synth_f32_exact): pass when |y - S/k| <= rtol |S/k|, or
+    on the floor |y - S/k| <= rtol * F with F = sum|x| / k, the window's mean
+    absolute input (for |S/k| ~ 0).  Returns {"checked", "mismatches",
+    "first_bad", "floor_used" (outputs that passed only on the floor),
+    "not_correctly_rounded" (y != fl32(S/k)), "max_rel" (over S != 0),
+    "max_cond" (max |y - S/k| / F; the fp32 output rounding alone is up to
+    2^-24)}."""
+    threads = threads or min(16, len(os.sched_getaffinity(0)))
+    y = np.ascontiguousarray(y, dtype=np.float32)
+    st = np.zeros(4, np.uint64)
+    ds = np.zeros(2, np.float64)
+    rc = _load().oracle_check_synth_f32_exact(_ptr(y), y.size, channels, k, seed, offset, dist, rtol, threads,
+                                             _ptr(st), _ptr(ds))
+    if rc == -2:
+        raise ValueError("check_synth_exact: a sample is not a multiple of 2^-64 (not exactly representable)")
+    if rc != 0:
+        raise ValueError(f"check_synth_exact: bad arguments (n={y.size}, C={channels}, k={k}, offset={offset})")
+    return {"checked": int(y.size), "mismatches": int(st[0]), "first_bad": None if st[0] == 0 else int(st[1]),
+            "floor_used": int(st[2]), "not_correctly_rounded": int(st[3]), "max_rel": float(ds[0]),
+            "max_cond": float(ds[1])}
+
+
+def numpy_synth_f32_dist2(n: int, seed: int = 0x5EED, offset: int = 0) -> np.ndarray:
+    """Independent numpy statement of the dist-2 generator (cross-check of
+    synth_f32_dist2 in mavg_oracle.c; shares no code with it)."""
+    z = np.arange(offset, offset + n, dtype=np.uint64) + np.uint64(seed)
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    h = z ^ (z >> np.uint64(31))
+    m = np.uint64(0x3FFF)
+    i = sum(((h >> np.uint64(s)) & m).astype(np.int64) for s in (0, 14, 28, 42)) - 32766
+    b = ((h >> np.uint64(56)) & np.uint64(31)).astype(np.int64)
+    s = np.where(b < 8, 0, b - 8)
+    v = i.astype(np.float64) * (1.0 / 3000.0)
+    return (v * np.ldexp(1.0, -s)).astype(np.float32)

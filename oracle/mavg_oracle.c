@@ -109,13 +109,47 @@ int oracle_window_sum_i64(const int16_t* x, size_t n, int C, int k,
  * x[i] = (int16)(splitmix64(seed + i) >> 48); the GPU generator in
  * libmavg computes the identical sequence so any sub-range can be regenerated
  * on the host.  dist 0: int16-valued; dist 1: uniform [0,1) with 24-bit
- * mantissa (precision stress, parity tests only). */
+ * mantissa (precision stress, parity tests only); dist 2: zero-mean,
+ * mixed-scale, non-dyadic fp32 (synth_f32_dist2: rounding and cancellation
+ * stress at full size). */
 static inline uint64_t splitmix64(uint64_t z)
 {
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+
+/* dist 2.  i = (sum of the four 14-bit fields of h) - 32766: an Irwin-Hall
+ * integer in [-32766, 32766], symmetric about 0.  v = fl64(i * fl64(1/3000))
+ * (a full 24-bit fp32 mantissa after rounding: the values are not dyadic
+ * fractions with short expansions), scaled by 2^-s with s = max(0, b - 8), b
+ * the 5 bits above the fields (a quarter of the samples at full scale, the rest
+ * spread over 2^-1 .. 2^-23), then rounded to fp32.  Window sums then mix
+ * magnitudes 2^3 .. 2^-35 and cancel towards 0, so fp64 accumulation rounds.
+ * Every step is one correctly rounded IEEE operation (no fused or reassociated
+ * arithmetic), so the device generator (synth_kernel) matches it bit for bit.
+ * Smallest non-zero |x| is 2^-23/3000 > 2^-41: x * 2^64 is an integer (the
+ * exact checker below relies on it). */
+static inline float synth_f32_dist2(uint64_t h)
+{
+    const int64_t i = (int64_t)(h & 0x3fffu) + (int64_t)((h >> 14) & 0x3fffu) +
+                      (int64_t)((h >> 28) & 0x3fffu) + (int64_t)((h >> 42) & 0x3fffu) - 32766;
+    const int b = (int)((h >> 56) & 31u);
+    const int s = b < 8 ? 0 : b - 8;
+    uint64_t pbits = (uint64_t)(1023 - s) << 52;   /* 2^-s, exactly */
+    double p;
+    memcpy(&p, &pbits, sizeof p);
+    const double v = (double)i * (1.0 / 3000.0);
+    return (float)(v * p);
+}
+
+static inline float synth_f32_at(uint64_t seed, uint64_t i, int dist)
+{
+    uint64_t h = splitmix64(seed + i);
+    if (dist == 1) return (float)(h >> 40) * (1.0f / 16777216.0f);
+    if (dist == 2) return synth_f32_dist2(h);
+    return (float)(int16_t)(uint16_t)(h >> 48);
 }
 
 void oracle_synth_i16(int16_t* x, size_t n, uint64_t seed, uint64_t offset)
@@ -126,11 +160,7 @@ void oracle_synth_i16(int16_t* x, size_t n, uint64_t seed, uint64_t offset)
 
 void oracle_synth_f32(float* x, size_t n, uint64_t seed, uint64_t offset, int dist)
 {
-    for (size_t i = 0; i < n; ++i) {
-        uint64_t h = splitmix64(seed + offset + i);
-        if (dist == 1) x[i] = (float)(h >> 40) * (1.0f / 16777216.0f);
-        else           x[i] = (float)(int16_t)(uint16_t)(h >> 48);
-    }
+    for (size_t i = 0; i < n; ++i) x[i] = synth_f32_at(seed, offset + i, dist);
 }
 
 /* ---- multi-core CPU baseline --------------------------
@@ -179,13 +209,8 @@ int oracle_mavg_f32_mt(const float* x, float* y, size_t n, int C, int k, int thr
  * integers, and every fp64 partial sum of dist-0 (int16-valued) or dist-1
  * (multiples of 2^-24 below 1) samples is a multiple of 2^-24 below 2^29 in
  * magnitude for k < 2^29, so fp64 adds them without rounding in any order.
- * Used by the -m gpu full-size parity tests (every output of a 2^30 launch). */
-static inline float synth_f32_at(uint64_t seed, uint64_t i, int dist)
-{
-    uint64_t h = splitmix64(seed + i);
-    return dist == 1 ? (float)(h >> 40) * (1.0f / 16777216.0f) : (float)(int16_t)(uint16_t)(h >> 48);
-}
-
+ * Used by the -m gpu full-size parity tests (every output of a 2^30 launch).
+ * dist 2 (inexact in fp64) has its own checker: oracle_check_synth_f32_exact. */
 int oracle_check_synth_f32(const float* y, size_t n, int C, int k, uint64_t seed, uint64_t offset,
                            int dist, double rtol, int threads,
                            uint64_t* n_bad, uint64_t* first_bad, double* max_rel)
@@ -230,6 +255,128 @@ int oracle_check_synth_f32(const float* y, size_t n, int C, int k, uint64_t seed
     *n_bad = bad_total;
     *first_bad = first;
     *max_rel = worst;
+    return 0;
+}
+
+/* ---- exact fp32 checker (any dist) -----------------------------------------
+ * The reference loop (profilable_moving_averager.cpp:27-35) keeps a running
+ * sum; in fp32 mode its fp64 running sum rounds once the samples are not
+ * small integers (dist 2), and over 2^30 steps that drift is not a usable
+ * yardstick.  This checker uses the EXACT window sum instead: every sample is
+ * an integer multiple of 2^-64 below 2^32 in magnitude (checked: the function
+ * returns -2 otherwise), so S = sum of x * 2^64 is exact in __int128 (|S| <
+ * 2^96 * 2^27 for k < 2^27).  want = S / k (one fp64 rounding of S, one of the
+ * quotient: relative error < 2^-52).  For each output:
+ *   err <= rtol * |want|                  passes (relative bar, north_star)
+ *   else err <= rtol * F, F = sum|x| / k  passes on the floor (|want| ~ 0:
+ *                                         the window's mean absolute input),
+ *                                         counted in stats[2]
+ *   else                                  a mismatch (stats[0], first in stats[1]).
+ * stats[3] counts outputs that are not the correctly rounded fp32 of want.
+ * dstats[0] = max err / |want| over want != 0; dstats[1] = max err / F (the
+ * error against the summation's condition scale: fp32 output rounding alone
+ * contributes up to 2^-24). */
+static inline int fx64(float x, __int128* out)
+{
+    uint32_t u;
+    memcpy(&u, &x, sizeof u);
+    const int e = (int)((u >> 23) & 0xffu);
+    if (e == 255) return -1;                             /* inf / NaN */
+    const int64_t m = e ? (int64_t)((u & 0x7fffffu) | 0x800000u) : (int64_t)(u & 0x7fffffu);
+    const int sh = (e ? e : 1) - 150 + 64;               /* x = m 2^(e-150): x 2^64 = m 2^sh */
+    __int128 v;
+    if (m == 0) { *out = 0; return 0; }
+    if (sh >= 0) {
+        if (sh > 72) return -1;                          /* |x| >= 2^32: the window sums could overflow */
+        v = (__int128)m << sh;
+    } else {
+        if (sh < -24 || (m & ((INT64_C(1) << -sh) - 1)) != 0) return -1;   /* not a multiple of 2^-64 */
+        v = (__int128)(m >> -sh);
+    }
+    *out = (u >> 31) ? -v : v;
+    return 0;
+}
+/* (double) of an __int128 without the library call: two exact halves, one
+ * rounding each (relative error < 2^-52) */
+static inline double i128_to_double(__int128 s)
+{
+    const int64_t hi = (int64_t)(s >> 64);
+    const uint64_t lo = (uint64_t)s;
+    return (double)hi * 0x1p64 + (double)lo;
+}
+
+int oracle_check_synth_f32_exact(const float* y, size_t n, int C, int k, uint64_t seed, uint64_t offset,
+                                 int dist, double rtol, int threads, uint64_t* stats, double* dstats)
+{
+    if (C < 1 || C > ORACLE_MAX_CH || k < 1 || k >= (1 << 27) || (n % (size_t)C) != 0 ||
+        (offset % (uint64_t)C) != 0 || threads < 1 || dist < 0 || dist > 2)
+        return -1;
+    const size_t frames = n / (size_t)C;
+    const uint64_t g0 = offset / (uint64_t)C;
+    const double dk = (double)k;
+    uint64_t bad_total = 0, first = UINT64_MAX, floor_total = 0, ncr_total = 0;
+    double worst_rel = 0.0, worst_cond = 0.0;
+    int failed = 0;
+#pragma omp parallel for num_threads(threads) schedule(static) reduction(+ : bad_total, floor_total, ncr_total) \
+    reduction(min : first) reduction(max : worst_rel, worst_cond, failed)
+    for (int t = 0; t < threads; ++t) {
+        const size_t f0 = frames * (size_t)t / (size_t)threads;
+        const size_t f1 = frames * (size_t)(t + 1) / (size_t)threads;
+        int fail_t = 0;
+        for (int ch = 0; ch < C && !fail_t; ++ch) {
+            const uint64_t g = g0 + f0;
+            const uint64_t lo = g >= (uint64_t)k ? g - (uint64_t)k : 0;
+            __int128 s = 0, sa = 0, v;
+            for (uint64_t j = lo; j < g; ++j) {
+                if (fx64(synth_f32_at(seed, j * C + ch, dist), &v)) { fail_t = 1; break; }
+                s += v;
+                sa += v < 0 ? -v : v;
+            }
+            for (size_t f = f0; f < f1 && !fail_t; ++f) {
+                const uint64_t gf = g0 + f;
+                if (fx64(synth_f32_at(seed, gf * C + ch, dist), &v)) { fail_t = 1; break; }
+                s += v;
+                sa += v < 0 ? -v : v;
+                if (gf >= (uint64_t)k) {
+                    if (fx64(synth_f32_at(seed, (gf - k) * C + ch, dist), &v)) { fail_t = 1; break; }
+                    s -= v;
+                    sa -= v < 0 ? -v : v;
+                }
+                const double want = i128_to_double(s) * 0x1p-64 / dk;
+                const double fl = i128_to_double(sa) * 0x1p-64 / dk;
+                const double got = (double)y[f * C + ch];
+                const double err = fabs(got - want);
+                const uint64_t idx = (uint64_t)(f * C + ch);
+                if (err <= rtol * fabs(want)) {
+                    /* relative bar */
+                } else if (err <= rtol * fl) {
+                    ++floor_total;
+                } else {            /* also NaN */
+                    ++bad_total;
+                    if (idx < first) first = idx;
+                }
+                if ((float)want != (float)got) ++ncr_total;
+                if (want != 0.0) {
+                    const double r = err / fabs(want);
+                    if (r > worst_rel || r != r) worst_rel = r != r ? INFINITY : r;
+                }
+                if (fl > 0.0) {
+                    const double r = err / fl;
+                    if (r > worst_cond || r != r) worst_cond = r != r ? INFINITY : r;
+                } else if (err != 0.0) {
+                    worst_cond = INFINITY;
+                }
+            }
+        }
+        if (fail_t) failed = 1;
+    }
+    if (failed > 0) return -2;
+    stats[0] = bad_total;
+    stats[1] = first;
+    stats[2] = floor_total;
+    stats[3] = ncr_total;
+    dstats[0] = worst_rel;
+    dstats[1] = worst_cond;
     return 0;
 }
 

@@ -89,6 +89,8 @@ def test_fill_synthetic_validates():
     assert lib.mavg_fill_synthetic(None, 0, _lib.F32, 1, 0, 0, None) == _lib.OK
     assert lib.mavg_fill_synthetic(None, 8, _lib.F32, 1, 0, 0, None) == _lib.ERR_INVALID_ARG
     assert lib.mavg_fill_synthetic(16, 8, _lib.I16, 1, 0, 1, None) == _lib.ERR_INVALID_ARG
+    assert lib.mavg_fill_synthetic(16, 8, _lib.I16, 1, 0, 2, None) == _lib.ERR_INVALID_ARG  # dist 2: fp32 only
+    assert lib.mavg_fill_synthetic(16, 8, _lib.F32, 1, 0, 3, None) == _lib.ERR_INVALID_ARG
 
 
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):
@@ -202,3 +204,23 @@ def test_block_size_tuned_and_fallback_geometry():
     assert dsp.plan(1 << 20, 70_000, block_size=512).startswith("ahead_scan<")
     with pytest.raises(dsp.MavgError):
         dsp.plan(1 << 20, 64, block_size=48)
+
+
+def test_workspace_error_on_misaligned_view_queues_nothing():
+    """A view 4 B past 16-B alignment peels a 3-frame head (frame-unit form)
+    before the vector body.  A workspace that covers the head's look-ahead
+    launch (32 B) but not the body's must be refused before anything is
+    queued: both launches are planned first (mavg.h)."""
+    lib = _lib.load()
+    din, dout, ws = (1 << 20) + 4, (1 << 21) + 4, 1 << 22
+    st = lib.mavg_run(din, dout, 1 << 20, 1, 70_000, _lib.F32, _lib.ALGO_BLELLOCH, 0, None, ws, 32, None)
+    assert st == _lib.ERR_WORKSPACE
+
+
+def test_direct_block_size_falls_back_when_the_halo_does_not_fit():
+    import digital_signal_processsing_amd as dsp
+    # fp32 mono k=13000: a 1024-thread direct tile would need > 64 KiB of LDS;
+    # the tuned 2-unit x 256-thread launch runs instead
+    p = dsp.plan(1 << 20, 13_000, algo="direct", block_size=1024)
+    assert p == dsp.plan(1 << 20, 13_000, algo="direct") and "U=2" in p and "block=256" in p, p
+    assert "block=1024" in dsp.plan(1 << 20, 1000, algo="direct", block_size=1024)

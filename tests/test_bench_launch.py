@@ -68,3 +68,8 @@ def test_bench_self_launch_two_ranks_gloo_check(gpu):
     assert d["check"]["ranks"] == 2 and d["check"]["mismatches"] == 0 and d["check"]["slices"] > 0
     assert "interior launch" in d["roofline"]["scope"]
     assert d["value"] > 0 and d["scaling"] == "weak"
+    sd = d["scaling_detail"]
+    assert 0 < sd["weak_scaling_efficiency"] <= 1.2, sd
+    assert [r["rank"] for r in sd["per_rank"]] == [0, 1]
+    for r in sd["per_rank"]:
+        assert r["halo_wait_ms"] >= 0 and r["head_ms"] > 0 and r["single_launch_gsamples_s"] > 0, r

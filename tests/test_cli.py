@@ -265,8 +265,79 @@ def test_gpu_bins_run_the_argv_block_size(tmp_path, stereo_wav, oracle_mod, name
     path, data = stereo_wav
     r = _run(name, path, 41, block, "--out", tmp_path / "o.wav", cwd=tmp_path)
     assert r.returncode == 0, r.stdout + r.stderr
-    kern = [l for l in r.stdout.splitlines() if l.startswith("Kernel: ")]
+    kern = [l for l in r.stderr.splitlines() if l.startswith("Kernel: ")]  # stderr: stdout is the reference report
     assert kern and re.search(r"block=(\d+)", kern[0]).group(1) == str(want), kern
     assert np.array_equal(rb.read_wav_samples(str(tmp_path / "o.wav")), oracle_mod.mavg_i16(data.reshape(-1), 41, 2))
     rows = list(csv.reader(open(tmp_path / "benchmark_data.csv")))
     assert rows[1][4] == str(block)
+
+
+# The reference's stdout, line by line: the variant's header (if it prints one:
+# hillis_steele_averager.cu:205-207, profilable_parallel_averager.cu:118-121,
+# profilable_sm_averager.cu:141-144), then per memory mode the mode line
+# (e.g. blelloch_scan_averager.cu:237,266) and ProfileResult::print_stats
+# (benchmark.h:47-68; the H2D / D2H lines only when those phases took time).
+_NUM = r"-?[0-9]+\.[0-9]{3}"
+_STATS = [r"1\. LATENCY BREAKDOWN \(Steady State\)", rf"?   H2D Transfer:   {_NUM} ms",
+          rf"   Kernel Compute: {_NUM} ms", rf"?   D2H Transfer:   {_NUM} ms", r"   -----------------------------",
+          rf"   TOTAL LATENCY:  {_NUM} ms", r"", r"2\. THROUGHPUT \(Steady State\)",
+          rf"   Kernel Bandwidth: {_NUM} GB/s", rf"   Kernel Speed:   {_NUM} Mega Samples/s",
+          rf"   App BandWidth:   {_NUM} GB/s", rf"   App Speed:      {_NUM} Mega Samples/s",
+          rf"   Cold Start:     {_NUM} Mega Samples/s \(Includes Init\)", r"", r"3\. INITIALIZATION COST \(One-time\)",
+          rf"   Allocation:     {_NUM} ms", rf"   First Frame:    {_NUM} ms \(Cold Start\)",
+          r"___________________________________", r""]
+_HEADERS = {
+    "bin_parallel": [r"--- SIMPLE PARALLEL AVERAGER ---", r"Samples: 12002", r"point: 41", r"block Size: 96"],
+    "bin_shared": [r"--- SHARED MEMORY PARALLEL AVERAGER ---", r"Samples: 12002", r"point: 41", r"block Size: 96"],
+    "bin_hillis": [r"--- Hillis Steele Averager ---", r"total samples: 12002", r"point: 41"],
+}
+
+
+def _report_template(name):
+    lines = list(_HEADERS.get(name, []))
+    for mode in (r"--- MEM MODE: STANDARD \(Discrete\) ---", r"--- MODE: UNIFIED \(Zero-Copy\) ---"):
+        lines += [r"", mode] + _STATS
+    return lines + [r">> Data saved to benchmark_data\.csv"]   # CsvLogger's destructor, gpu_utils.h:230
+
+
+def _match_report(stdout, template):
+    """Match stdout line by line; a template line starting with '?' is optional."""
+    import re
+    out = stdout.split("\n")
+    i = 0
+    for pat in template:
+        optional = pat.startswith("?")
+        pat = pat[1:] if optional else pat
+        if i < len(out) and re.fullmatch(pat, out[i]):
+            i += 1
+        elif not optional:
+            return f"line {i}: {out[i] if i < len(out) else '<eof>'!r} does not match {pat!r}"
+    rest = [l for l in out[i:] if l != ""]
+    return None if not rest else f"trailing output: {rest[:3]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", GPU_BINS)
+def test_gpu_bins_stdout_is_the_reference_report(tmp_path, stereo_wav, name):
+    """stdout carries nothing but the reference's report, in its order (the
+    launch description goes to stderr)."""
+    path, _ = stereo_wav
+    r = _run(name, path, 41, 96, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    err = _match_report(r.stdout, _report_template(name))
+    assert err is None, f"{name}: {err}\n{r.stdout}"
+    assert "Kernel: " in r.stderr
+
+
+def test_bin_cpu_stdout_is_the_reference_report(tmp_path, stereo_wav):
+    """bin_cpu's whole stdout against the reference's CPU averager report:
+    header (profilable_moving_averager.cpp:51-53), one stats block (:80),
+    the CSV logger's line (gpu_utils.h:230) -- and the matcher rejects extra
+    lines."""
+    path, _ = stereo_wav
+    r = _run("bin_cpu", path, 41, 96, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    tmpl = [r"--- Single Thread Averager ---", r"total samples: 12002", r"point: 41"] + _STATS + [
+        r">> Data saved to benchmark_data\.csv"]
+    assert _match_report(r.stdout, tmpl) is None, r.stdout
+    assert _match_report(r.stdout + "Kernel: x\n", tmpl) is not None

@@ -47,6 +47,32 @@ def test_every_output_matches_oracle(oracle_mod, gpu, name, n, k, C, dt, algo):
         assert r["max_rel"] == 0.0, f"{name}: {r}"
 
 
+# fp32 parity on rounding, cancelling data at full size (dist 2: zero-mean,
+# mixed-scale, non-dyadic samples whose fp64 window sums round): every output
+# against the EXACT window sum (__int128 fixed point, oracle.check_synth_exact).
+# Bar (north_star, DESIGN.md "Parity bar"): |y - S/k| <= 1e-5 |S/k|, or, where
+# the sum cancels to ~0, <= 1e-5 * F with F = sum|x|/k the window's mean
+# absolute input (the count of such outputs is reported); and the error beyond
+# the fp32 output rounding must stay under 1e-9 F (fp64 accumulation quality).
+DIST2_CONFIGS = [c for c in CONFIGS if c[4] == "f32"]
+
+
+@pytest.mark.parametrize("name,n,k,C,dt,algo", DIST2_CONFIGS, ids=[c[0] + "_dist2" for c in DIST2_CONFIGS])
+def test_every_output_of_rounding_data_within_bar(oracle_mod, gpu, name, n, k, C, dt, algo):
+    import torch
+    import digital_signal_processsing_amd as dsp
+    x = dsp.fill_synthetic(n, torch.float32, seed=SEED, dist=2, device=gpu)
+    y = dsp.moving_average(x, k, channels=C, algo=algo)
+    del x
+    yh = y.cpu().numpy()
+    del y
+    r = oracle_mod.check_synth_exact(yh, k, C, seed=SEED, dist=2, rtol=RTOL)
+    print(f"{name} dist2: {r}")
+    assert r["checked"] == n
+    assert r["mismatches"] == 0, f"{name}: {r}"
+    assert r["max_cond"] <= 2.0 ** -24 + 1e-9, f"{name}: {r}"
+
+
 @pytest.mark.parametrize("world", [2, 8])
 def test_every_output_of_sharded_weak_scaling_signal(oracle_mod, gpu, world):
     """BASELINE config #5 on one GPU: the 2^30-sample shards of a world*2^30

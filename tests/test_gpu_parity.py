@@ -41,9 +41,10 @@ def test_device_synth_matches_oracle(oracle_mod, gpu):
     import digital_signal_processsing_amd as dsp
     import torch
     n = 100_003
-    for dist in (0, 1):
+    for dist in (0, 1, 2):
         y = dsp.fill_synthetic(n, torch.float32, seed=0x5EED, offset=999, dist=dist, device=gpu)
-        assert np.array_equal(y.cpu().numpy(), oracle_mod.synth_f32(n, seed=0x5EED, offset=999, dist=dist))
+        assert np.array_equal(y.cpu().numpy().view(np.uint32),
+                              oracle_mod.synth_f32(n, seed=0x5EED, offset=999, dist=dist).view(np.uint32)), dist
     y = dsp.fill_synthetic(n, torch.int16, seed=7, offset=3, device=gpu)
     assert np.array_equal(y.cpu().numpy(), oracle_mod.synth_i16(n, seed=7, offset=3))
 
@@ -90,6 +91,31 @@ def test_ragged_sizes_f32(oracle_mod, gpu, algo, frames):
         x = oracle_mod.synth_f32(frames * C, offset=frames + k, dist=dist)
         assert_f32_close(_run(x, k, C, algo, gpu), oracle_mod.mavg_f32(x, k, C),
                          f"{algo} frames={frames} C={C} k={k} dist={dist}")
+
+
+# fp32 rounding data (dist 2: zero-mean, mixed-scale, non-dyadic; its fp64
+# window sums round) against the EXACT window sum, every algorithm and kernel
+# family: the 1e-5 relative bar, with the floor 1e-5 * (window's mean |x|)
+# for outputs whose sum cancels to ~0, and the error beyond the fp32 output
+# rounding held under 1e-9 of that scale (oracle.check_synth_exact)
+ROUNDING_CASES = [  # frames, C, k
+    (1, 1, 1), (63, 1, 7), (4097, 2, 41), (65_537, 1, 1024), (100_003, 1, 4096), (300_007, 1, 20_000),
+    (300_007, 2, 44_100), (200_003, 3, 333), (1_000_003, 1, 70_000)]
+
+
+@pytest.mark.parametrize("algo", ALL_ALGOS)
+def test_rounding_data_against_exact_sums(oracle_mod, gpu, algo):
+    import digital_signal_processsing_amd as dsp
+    import torch
+    for frames, C, k in ROUNDING_CASES:
+        if algo == "naive" and frames * k > 50_000_000:
+            continue
+        if algo.startswith("direct") and k > 5000:
+            continue  # the direct kernel's LDS halo (its reference is a small-window path)
+        x = dsp.fill_synthetic(frames * C, torch.float32, dist=2, device=gpu)
+        y = dsp.moving_average(x, k, channels=C, algo=algo).cpu().numpy()
+        r = oracle_mod.check_synth_exact(y, k, C, dist=2, rtol=RTOL)
+        assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, (algo, frames, C, k, r)
 
 
 @pytest.mark.parametrize("C", [1, 2, 3, 4, 5, 6, 7, 8])
@@ -255,11 +281,14 @@ def test_many_channels_auto(oracle_mod, gpu):
 
 
 # ---------------------------------------------------------------------------
-# look-ahead scan (long windows): carry from whole-tile records published
-# inside the launch (mavg_lookback.hpp)
+# the long-window scan: the chained look-back scan (mavg_chain.hpp), carry
+# from the nearest published inclusive prefix plus the aggregates above it
+LONG_KERNEL = "chain_scan"
+
+
 def _lookback_tile(dsp, n, k, C, dt):
     plan = dsp.plan(n, k, C, dt)
-    assert plan.startswith("ahead_scan<"), plan
+    assert plan.startswith(LONG_KERNEL + "<"), plan
     return int(plan.split("tile_frames=")[1].split()[0])
 
 
@@ -274,7 +303,7 @@ def test_ahead_window_edges(oracle_mod, gpu, C, dtype):
     frames = 200_003
     T = _lookback_tile(dsp, frames * C, 70_001, C, dt)
     for k in sorted({16 * T - 1, 16 * T, 16 * T + 1, 20_000, 44_100, 70_001}):
-        if dsp.plan(frames * C, k, C, dt).split("<")[0] != "ahead_scan":
+        if dsp.plan(frames * C, k, C, dt).split("<")[0] != LONG_KERNEL:
             continue
         if dtype == "i16":
             x = oracle_mod.synth_i16(frames * C, offset=k + C)
@@ -344,7 +373,7 @@ def test_ahead_graph_capture(oracle_mod, gpu, own_workspace):
     n, k = 1_000_003, 30_000
     x = torch.from_numpy(oracle_mod.synth_f32(n, seed=23, dist=1)).to(gpu)
     y = torch.empty_like(x)
-    assert dsp.plan(n, k).startswith("ahead_scan<")
+    assert dsp.plan(n, k).startswith(LONG_KERNEL + "<")
     ws = torch.empty(dsp.workspace_bytes(n, k), dtype=torch.uint8, device=gpu) if own_workspace else None
     s = torch.cuda.Stream(device=gpu)
     s.wait_stream(torch.cuda.current_stream(gpu))
@@ -392,7 +421,10 @@ def test_ahead_large_stereo_slices(oracle_mod, gpu):
 
 
 def _with_schedule(sched, fn):
-    """Run fn under a forced look-ahead schedule (mavg_test_ahead_schedule)."""
+    """Run fn under a forced chain schedule (mavg_test_ahead_schedule: `slots`
+    = how many predecessors a tile searches for a published inclusive before
+    it recomputes the run's chain from its seed, `spin` = polls before a
+    missing link or record is recomputed)."""
     from digital_signal_processsing_amd import _lib
     lib = _lib.load()
     lib.mavg_test_ahead_schedule(sched.get("slots", -1), sched.get("spin", -1))
@@ -405,33 +437,32 @@ def _with_schedule(sched, fn):
 @pytest.mark.parametrize("dtype,C,k", [("f32", 1, 20_000), ("f32", 3, 9_000), ("i16", 2, 44_100),
                                        ("i16", 1, 100_000), ("f32", 1, 300_000), ("f32", 2, 600_000),
                                        ("f32", 1, 1_100_000), ("i16", 1, 2_200_000)])
-def test_ahead_records_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, k):
-    """Every record is the same bits whether its producer published it (look-
-    ahead D slots, head duty, own tile) or the consumer recomputed it after a
-    bounded wait: forcing the recompute path (SPIN=0), the one-pass form
-    (SLOTS=0: every tile publishes only its own records), minimal and absent
-    look-ahead gives bitwise the same output as the default schedule, also for
-    fp32 data whose sums round (uniform [0,1) values), and it matches the
-    oracle.  Signal lengths give ragged XCD runs (tiles not a multiple of 8)."""
+def test_long_window_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, k):
+    """The chain value is the strict left fold seed + D(rs) + ... + D(t-1),
+    whichever path computes it: a published inclusive plus the aggregates
+    above it (default), every missing aggregate and seed record recomputed by
+    the waiting wave (SPIN=0), the whole run's chain refolded from its seed by
+    every tile (SLOTS=0), or only the nearest predecessor searched (SLOTS=1)
+    -- bitwise the same output, on fp32 data whose sums round (dist 2, checked
+    against the exact window sums) and on int16 (bit-exact with the oracle).
+    Signal lengths give ragged XCD runs (tiles not a multiple of 8); the
+    windows span 2 .. 500 tiles, so the run seeds need many head-duty records."""
     import digital_signal_processsing_amd as dsp
     dt = dsp.F32 if dtype == "f32" else dsp.I16
-    frames = 2_600_000 // C + 12_345  # > D = 512 tiles at C=1: the look-ahead producers run
+    frames = 2_600_000 // C + 12_345
     plan = dsp.plan(frames * C, k, C, dt)
-    assert plan.startswith("ahead_scan<")
-    # mono windows whose per-wave records fit one round of loads take the
-    # per-wave records (wrec=1); the others one record per tile
-    tf = int(plan.split("tile_frames=")[1].split()[0])
-    assert ("wrec=1" in plan) == (C == 1 and k // tf + 1 <= 64), plan
+    assert plan.startswith(LONG_KERNEL + "<"), plan
     if dtype == "f32":
-        x = oracle_mod.synth_f32(frames * C, seed=77, dist=1)
+        x = oracle_mod.synth_f32(frames * C, seed=77, dist=2)
     else:
         x = oracle_mod.synth_i16(frames * C, seed=77)
     base = _run(x, k, C, "auto", gpu)
-    for sched in ({"spin": 0}, {"slots": 0}, {"slots": 8}, {"slots": 1 << 28}, {"slots": 8, "spin": 0}):
+    for sched in ({"spin": 0}, {"slots": 0}, {"slots": 1}, {"slots": 1 << 28}, {"slots": 0, "spin": 0}):
         y = _with_schedule(sched, lambda: _run(x, k, C, "auto", gpu))
         assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), sched
     if dtype == "f32":
-        assert_f32_close(base, oracle_mod.mavg_f32(x, k, C), f"C={C} k={k}")
+        r = oracle_mod.check_synth_exact(base, k, C, seed=77, dist=2, rtol=RTOL)
+        assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, r
     else:
         assert np.array_equal(base, oracle_mod.mavg_i16(x, k, C))
 
@@ -457,8 +488,8 @@ def test_ahead_poisoned_workspace(oracle_mod, gpu, fill):
 
 
 def test_ahead_deterministic_repeats(oracle_mod, gpu):
-    """Repeated launches of the look-ahead scan on fp32 data whose sums round:
-    bitwise identical outputs (records are summed in a fixed order)."""
+    """Repeated launches of the long-window scan on fp32 data whose sums round:
+    bitwise identical outputs (the chain is one fixed left fold)."""
     import digital_signal_processsing_amd as dsp
     import torch
     n, k = 1 << 24, 50_000

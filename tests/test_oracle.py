@@ -140,8 +140,81 @@ def test_full_signal_checker_equals_serial_loop(oracle_mod, C, k, dist, offset, 
 
 def test_full_signal_checker_rejects_bad_args(oracle_mod):
     y = np.zeros(10, np.float32)
-    for kw in (dict(k=0), dict(k=3, channels=3), dict(k=3, channels=2, offset=1), dict(k=3, dist=2)):
+    for kw in (dict(k=0), dict(k=3, channels=3), dict(k=3, channels=2, offset=1), dict(k=3, dist=3)):
         with pytest.raises(ValueError):
             oracle_mod.check_synth(y, **kw)
     with pytest.raises(TypeError):
         oracle_mod.check_synth(np.zeros(4, np.float64), 3)
+
+
+def test_dist2_generator_matches_numpy_statement(oracle_mod):
+    """The zero-mean, mixed-scale generator (fp32 rounding stress): C and an
+    independent numpy statement agree bit for bit at any offset."""
+    for off in (0, 12345, (1 << 40) + 7):
+        a = oracle_mod.synth_f32(50_000, offset=off, dist=2)
+        b = oracle_mod.numpy_synth_f32_dist2(50_000, offset=off)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), off
+    x = oracle_mod.synth_f32(1 << 20, dist=2)
+    assert abs(float(x.mean())) < 0.01 and 1.5 < float(x.std()) < 2.0          # zero-mean
+    assert (x < 0).mean() > 0.45 and (np.abs(x) < 1e-3).mean() > 0.3           # both signs, mixed scale
+    assert np.abs(x[x != 0]).min() > 2.0 ** -41                                # exact in 2^-64 fixed point
+
+
+def test_dist2_fp64_window_sums_round(oracle_mod):
+    """dist 2 exists to make fp64 accumulation round: sequential fp64 window
+    sums differ from the exact (math.fsum) sums for a good share of windows,
+    so a full-size fp32 check on it is not a bit-equality check in disguise."""
+    import math
+    x = oracle_mod.synth_f32(1 << 16, dist=2).astype(np.float64)
+    k = 1024
+    inexact = 0
+    for s in range(0, len(x) - k, 257):
+        w = x[s:s + k]
+        acc = 0.0
+        for v in w:
+            acc += v
+        inexact += acc != math.fsum(w)
+    assert inexact > 50, inexact
+
+
+@pytest.mark.parametrize("C,k,dist,offset,threads", [
+    (1, 1024, 2, 0, 7), (2, 41, 2, 6, 3), (1, 7, 2, 12345, 8), (1, 44_100, 2, 0, 5), (3, 300, 1, 99 * 3, 4),
+    (1, 64, 0, 0, 2)])
+def test_exact_checker_accepts_restatement_and_flags_errors(oracle_mod, C, k, dist, offset, threads):
+    """check_synth_exact (exact __int128 window sums) accepts the serial fp64
+    restatement's output on every distribution -- its running-sum drift stays
+    far inside 1e-5 -- and reports an output nudged by more than the bar."""
+    n = 120_001 * C
+    x = oracle_mod.synth_f32(n + offset, dist=dist)
+    y = oracle_mod.mavg_f32(x, k, C)[offset:]
+    r = oracle_mod.check_synth_exact(y, k, C, offset=offset, dist=dist, threads=threads)
+    assert r["mismatches"] == 0 and r["checked"] == n, r
+    assert r["max_cond"] <= 2.0 ** -24 + 1e-9, r
+    i = n // 3
+    y[i] = np.float32(y[i] + 1e-4 * (abs(float(y[i])) + float(np.abs(x).mean())))  # > both bars
+    r = oracle_mod.check_synth_exact(y, k, C, offset=offset, dist=dist, threads=threads)
+    assert r["mismatches"] == 1 and r["first_bad"] == i, r
+    # NaN is a mismatch, never a pass
+    y[0] = np.nan
+    assert oracle_mod.check_synth_exact(y, k, C, offset=offset, dist=dist, threads=threads)["mismatches"] == 2
+
+
+def test_exact_checker_floor_for_cancelling_windows(oracle_mod):
+    """|S| ~ 0: an output off by less than 1e-5 of the window's mean absolute
+    input passes on the floor (and is counted), a larger error fails."""
+    k = 4
+    x = oracle_mod.synth_f32(4000, dist=2)
+    y = oracle_mod.mavg_f32(x, k, 1)
+    s = np.array([math_fsum(x[max(0, f - k + 1):f + 1]) for f in range(len(x))])
+    fl = np.array([np.abs(x[max(0, f - k + 1):f + 1].astype(np.float64)).sum() for f in range(len(x))]) / k
+    f = int(np.argmin(np.abs(s) / k / fl))          # the most cancelling window
+    y[f] = np.float32(s[f] / k + 0.5e-5 * fl[f])    # > 1e-5 |S/k|, < 1e-5 F
+    r = oracle_mod.check_synth_exact(y, k, 1, dist=2, threads=2)
+    assert r["mismatches"] == 0 and r["floor_used"] >= 1, r
+    y[f] = np.float32(s[f] / k + 2e-5 * fl[f])
+    assert oracle_mod.check_synth_exact(y, k, 1, dist=2, threads=2)["mismatches"] == 1
+
+
+def math_fsum(a):
+    import math
+    return math.fsum(a.astype(np.float64))

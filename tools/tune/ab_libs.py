@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--log2n", type=int, default=30)
     ap.add_argument("--algo", type=int, default=0, help="mavg_algo (0 auto, 5 direct)")
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--dist", type=int, default=0, help="synthetic distribution (fp32: 0, 1, 2)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--ypad", type=int, default=0, help="offset y by this many bytes inside a bigger buffer")
     ap.add_argument("--blocks", type=int, nargs=2, default=[0, 0],
@@ -39,7 +40,7 @@ def main():
     n = 1 << a.log2n
     tdt = torch.int16 if a.dtype == "i16" else torch.float32
     code = dsp.I16 if a.dtype == "i16" else dsp.F32
-    x = dsp.fill_synthetic(n, tdt, seed=0x5EED, device="cuda")
+    x = dsp.fill_synthetic(n, tdt, seed=0x5EED, dist=a.dist, device="cuda")
     pad = a.ypad // x.element_size()
     ybuf = torch.empty(n + pad, dtype=tdt, device="cuda")
     y = ybuf[pad:]
@@ -58,9 +59,18 @@ def main():
         libs.append((p, lib, buf.value.decode()))
         blocks[p] = a.blocks[li]
     stream = torch.cuda.current_stream().cuda_stream
+    wsb = {}
+    for p, lib, _ in libs:  # each library's own workspace (long-window scans)
+        nb = ctypes.c_size_t(0)
+        lib.mavg_workspace_bytes.argtypes = [ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
+        assert lib.mavg_workspace_bytes(n, a.c, a.k, code, a.algo, blocks[p], ctypes.byref(nb)) == 0
+        wsb[p] = torch.empty(max(16, nb.value), dtype=torch.uint8, device="cuda") if nb.value else None
 
     def launch(lib, p):
-        st = lib.mavg_run(x.data_ptr(), y.data_ptr(), n, a.c, a.k, code, a.algo, blocks[p], None, None, 0, stream)
+        ws = wsb[p]
+        st = lib.mavg_run(x.data_ptr(), y.data_ptr(), n, a.c, a.k, code, a.algo, blocks[p], None,
+                          ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0, stream)
         assert st == 0, st
 
     def copy():
@@ -97,7 +107,7 @@ def main():
     byt = 2 * x.element_size() * n
     print(f"n=2^{a.log2n} k={a.k} C={a.c} dtype={a.dtype} rounds={a.rounds} steps={a.steps} "
           f"y-x={y.data_ptr() - x.data_ptr():#x}  outputs equal: "
-          f"{bool(torch.equal(outs[0], outs[1]))}")
+          f"{bool(torch.equal(outs[0], outs[1]))}  max |diff| {float((outs[0].double() - outs[1].double()).abs().max()):.3g}")
     for p, lib, plan in libs + [("torch copy_", None, "")]:
         t = times[p]
         mean, med = statistics.mean(t), statistics.median(t)
