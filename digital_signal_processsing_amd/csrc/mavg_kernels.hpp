@@ -32,7 +32,6 @@
 // off on exact multiples.
 #pragma once
 
-#include "mavg_chain.hpp"
 #include "mavg_device.hpp"
 #include "mavg_direct.hpp"
 #include "mavg_lookback.hpp"

@@ -307,97 +307,6 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   return launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false>(sg, k, st, ws, C == 2 ? 768 : 1024);
 }
 
-// chained look-back scan (mavg_chain.hpp): zero the link and record
-// granules, then one launch; tile t publishes its aggregate D(t), folds the
-// nearest published inclusive prefix with the aggregates above it, and
-// publishes L(t).
-// Workspace (8-B granules, one block from the start, padded to 16 bytes for
-// the memset's fast form): aggregates and inclusive prefixes, one slot per
-// (tile, channel, 32-bit word of the accumulator), then the run seeds'
-// per-wave records (8 runs x (k/T + 2) tiles x 4 waves), then 16 bytes of
-// launch statistics (MAVG_AHEAD_STATS builds only).
-template <typename T, typename A, int C, int F, int U>
-struct ChainLayout {
-  using SA = typename ScanAcc<T, A>::type;
-  static constexpr int TF = kWG * F * U;
-  long long ntiles, hrec;
-  size_t link_gran, rec_gran;
-  ChainLayout(long long nframes, int k) {
-    ntiles = (nframes + TF - 1) / TF;
-    hrec = (long long)k / TF + 2;
-    link_gran = (size_t)ntiles * C * GranCount<A>::n;
-    rec_gran = (size_t)8 * hrec * kNW * C * GranCount<SA>::n;
-  }
-  size_t bytes() const { return ((2 * link_gran + rec_gran) * 8 + 15) / 16 * 16 + 16; }
-};
-template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, int DV = 0>
-int launch_chain_scan(const Sig& sg, int k, hipStream_t st, Workspace ws) {
-  const long long nframes = sg.nframes;
-  int reach = 1 << 30, spin = kAheadSpin;
-  {
-    const int t = g_test_ahead_slots.load(std::memory_order_relaxed);
-    if (t >= 0) reach = t;
-    const int s = g_test_ahead_spin.load(std::memory_order_relaxed);
-    if (s >= 0) spin = s;
-  }
-  constexpr int TF = kWG * F * U;
-  constexpr int VE = F * C;
-  constexpr int NSEG = U * kNW;
-  using SA = typename ScanAcc<T, A>::type;
-  constexpr size_t kStageBytes = (((size_t)(U * kWG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15;
-  const ChainLayout<T, A, C, F, U> L(nframes, k);
-  if (L.ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
-  const size_t need = L.bytes();
-  const size_t lds = kStageBytes + (size_t)NSEG * C * sizeof(SA) + (size_t)C * sizeof(A) + 8;
-  if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
-  if (g_plan) {
-    snprintf(g_plan->text, sizeof(g_plan->text),
-             "chain_scan<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d,rc=%d,dma=%d,dv=%d> grid=%lld block=%d lds=%zu "
-             "tile_frames=%d remap=1 ws=%zu",
-             type_name<T>(), type_name<A>(), C, F, U, NT, (int)RC, (int)DMA, DV, L.ntiles, kWG, lds, TF, need);
-    g_plan->ws_bytes = need;
-    return MAVG_OK;
-  }
-  if (ws.ptr == nullptr || ws.bytes < need) return MAVG_ERR_WORKSPACE;
-  if ((reinterpret_cast<uintptr_t>(ws.ptr) & 15u) != 0) return MAVG_ERR_MISALIGNED;
-  if (hipMemsetAsync(ws.ptr, 0, need, st) != hipSuccess) return MAVG_ERR_HIP;
-  unsigned long long* g = static_cast<unsigned long long*>(ws.ptr);
-  ChainParams p{};
-  p.in = sg.in;
-  p.out = sg.out;
-  p.hist = sg.hist;
-  p.nframes = nframes;
-  p.k = k;
-  p.halo_units = (k + F - 1) / F;
-  p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
-  p.hrec = (int)L.hrec;
-  p.spin = spin;
-  p.reach = reach;
-  p.pre = sg.pre;
-  p.eio = sg.eio;
-  p.agg = g;
-  p.inc = g + L.link_gran;
-  p.rec = g + 2 * L.link_gran;
-  p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
-  p.o = make_out_params(k);
-  hipLaunchKernelGGL((chain_scan_kernel<T, A, C, F, U, NT, RC, DMA, DV>), dim3((unsigned)L.ntiles), dim3(kWG), lds,
-                     st, p);
-  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
-}
-
-// The long-window scan: the chained look-back scan with 4096-frame tiles
-// (U=4 x 16-B units), LDS-DMA shifted stage, non-temporal shifted-tile loads
-// and output stores (its last use), default-policy tile loads (the tile is
-// the shifted tile of tile t + k/T, an L2 hit if it stays); fp32 mono keeps
-// the tile in registers across the barriers (RC).
-template <typename T, typename A, int C, int F>
-int dispatch_long(const Sig& sg, int k, hipStream_t st, Workspace ws) {
-  constexpr int U = 4;
-  constexpr int kNtA = kNtStore | kNtHalo;
-  constexpr bool kRC = sizeof(T) == 4 && C == 1;
-  return launch_chain_scan<T, A, C, F, U, kNtA, kRC, true>(sg, k, st, ws);
-}
-
 // segment streaming with the launch geometry measured best: short
 // XCD-remapped segments of at least 4 chunks and 4x the pre-roll (5.5-5.7
 // TB/s vs 5.0 for one long segment per workgroup, tools/tune/tune_scan.hip)
@@ -507,7 +416,7 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
       // fp32 halos past 16 KiB: the look-ahead scan beats the 1024-thread
       // tile (k=8192: 0.73 vs 0.69; k=12000: 0.71 vs 0.64, sweep_ahead.sh)
     }
-    return dispatch_long<T, A, C, F>(sg, k, st, ws);
+    return dispatch_ahead<T, A, C, F>(sg, k, st, ws);
   } else {
     // Hillis-Steele: the element-wise log-step scans make a tile's compute
     // long, so bigger tiles (fewer halos and barriers per byte) and the split

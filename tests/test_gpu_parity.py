@@ -281,9 +281,9 @@ def test_many_channels_auto(oracle_mod, gpu):
 
 
 # ---------------------------------------------------------------------------
-# the long-window scan: the chained look-back scan (mavg_chain.hpp), carry
-# from the nearest published inclusive prefix plus the aggregates above it
-LONG_KERNEL = "chain_scan"
+# the long-window scan: the look-ahead scan (mavg_lookback.hpp), carry from
+# whole-tile records published inside the launch
+LONG_KERNEL = "ahead_scan"
 
 
 def _lookback_tile(dsp, n, k, C, dt):
@@ -421,10 +421,7 @@ def test_ahead_large_stereo_slices(oracle_mod, gpu):
 
 
 def _with_schedule(sched, fn):
-    """Run fn under a forced chain schedule (mavg_test_ahead_schedule: `slots`
-    = how many predecessors a tile searches for a published inclusive before
-    it recomputes the run's chain from its seed, `spin` = polls before a
-    missing link or record is recomputed)."""
+    """Run fn under a forced look-ahead schedule (mavg_test_ahead_schedule)."""
     from digital_signal_processsing_amd import _lib
     lib = _lib.load()
     lib.mavg_test_ahead_schedule(sched.get("slots", -1), sched.get("spin", -1))
@@ -437,27 +434,30 @@ def _with_schedule(sched, fn):
 @pytest.mark.parametrize("dtype,C,k", [("f32", 1, 20_000), ("f32", 3, 9_000), ("i16", 2, 44_100),
                                        ("i16", 1, 100_000), ("f32", 1, 300_000), ("f32", 2, 600_000),
                                        ("f32", 1, 1_100_000), ("i16", 1, 2_200_000)])
-def test_long_window_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, k):
-    """The chain value is the strict left fold seed + D(rs) + ... + D(t-1),
-    whichever path computes it: a published inclusive plus the aggregates
-    above it (default), every missing aggregate and seed record recomputed by
-    the waiting wave (SPIN=0), the whole run's chain refolded from its seed by
-    every tile (SLOTS=0), or only the nearest predecessor searched (SLOTS=1)
-    -- bitwise the same output, on fp32 data whose sums round (dist 2, checked
-    against the exact window sums) and on int16 (bit-exact with the oracle).
-    Signal lengths give ragged XCD runs (tiles not a multiple of 8); the
-    windows span 2 .. 500 tiles, so the run seeds need many head-duty records."""
+def test_ahead_records_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, k):
+    """Every record is the same bits whether its producer published it (look-
+    ahead D slots, head duty, own tile) or the consumer recomputed it after a
+    bounded wait: forcing the recompute path (SPIN=0), the one-pass form
+    (SLOTS=0: every tile publishes only its own records), minimal and absent
+    look-ahead gives bitwise the same output as the default schedule, also for
+    fp32 data whose sums round and cancel (dist 2), and it matches the exact
+    window sums (fp32) / the oracle (int16).  Signal lengths give ragged XCD
+    runs (tiles not a multiple of 8)."""
     import digital_signal_processsing_amd as dsp
     dt = dsp.F32 if dtype == "f32" else dsp.I16
-    frames = 2_600_000 // C + 12_345
+    frames = 2_600_000 // C + 12_345  # > D = 512 tiles at C=1: the look-ahead producers run
     plan = dsp.plan(frames * C, k, C, dt)
-    assert plan.startswith(LONG_KERNEL + "<"), plan
+    assert plan.startswith("ahead_scan<")
+    # mono windows whose per-wave records fit one round of loads take the
+    # per-wave records (wrec=1); the others one record per tile
+    tf = int(plan.split("tile_frames=")[1].split()[0])
+    assert ("wrec=1" in plan) == (C == 1 and k // tf + 1 <= 64), plan
     if dtype == "f32":
         x = oracle_mod.synth_f32(frames * C, seed=77, dist=2)
     else:
         x = oracle_mod.synth_i16(frames * C, seed=77)
     base = _run(x, k, C, "auto", gpu)
-    for sched in ({"spin": 0}, {"slots": 0}, {"slots": 1}, {"slots": 1 << 28}, {"slots": 0, "spin": 0}):
+    for sched in ({"spin": 0}, {"slots": 0}, {"slots": 8}, {"slots": 1 << 28}, {"slots": 8, "spin": 0}):
         y = _with_schedule(sched, lambda: _run(x, k, C, "auto", gpu))
         assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), sched
     if dtype == "f32":
@@ -488,8 +488,8 @@ def test_ahead_poisoned_workspace(oracle_mod, gpu, fill):
 
 
 def test_ahead_deterministic_repeats(oracle_mod, gpu):
-    """Repeated launches of the long-window scan on fp32 data whose sums round:
-    bitwise identical outputs (the chain is one fixed left fold)."""
+    """Repeated launches of the look-ahead scan on fp32 data whose sums round:
+    bitwise identical outputs (records are summed in a fixed order)."""
     import digital_signal_processsing_amd as dsp
     import torch
     n, k = 1 << 24, 50_000

@@ -1,10 +1,26 @@
-// mavg_chain.hpp -- the chained look-back scan (chain_scan_kernel): windows too
-// long for an LDS-staged halo.  Replaces the carry of the reference's
-// recursive_blelloch (basics/blelloch_scan_averager.cu:134-167) and the
-// blelloch_uniform_add pass (:17-36) for any window length.
+// chain_experiment.hpp -- KEPT-OUT EXPERIMENT (round 3), not part of libmavg.
+//
+// The chained (decoupled) look-back scan for long windows: each tile scans
+// d = x - x[n-k] with its shifted tile staged in LDS, publishes its aggregate
+// D(t), and a dedicated fifth "chain" wave folds the nearest published
+// inclusive prefix with the aggregates above it (a strict left fold, so fp64
+// results are bitwise schedule-independent), then publishes L(t).  Correct:
+// every long-window parity test, the forced-schedule bitwise test and the
+// dist-2 rounding data passed on MI355X (profiles/r03_tuning/chain/).  Slow:
+// 0.25 of HBM peak against 0.68 for the look-ahead scan at 2^30 fp32,
+// k=44100.  The phase trace (MAVG_CHAIN_TRACE, chain_trace.py) shows why: the
+// look-back is one L2 round trip on data published by tiles running at the
+// same moment, 3.5-5.5 us under streaming load, added to every tile's
+// ~5-7 us of load + scan; tile lifetime doubles (9-12 us) and with ~5
+// workgroups per CU the bytes in flight halve.  The look-ahead scan issues its
+// record loads at the start of the tile, on records published D slots
+// earlier, so its carry costs no latency.  DESIGN.md "Tried this round".
+//
+// To rebuild it, include this file after mavg_launch.hpp in a tuning
+// translation unit and call dispatch_long<T, A, C, F>(...).
 #pragma once
 
-#include "mavg_lookback.hpp"
+#include "../../digital_signal_processsing_amd/csrc/mavg_launch.hpp"
 
 namespace mavg {
 
@@ -59,7 +75,9 @@ struct ChainParams {
   unsigned long long* agg;  // [ntiles][C][NGA] tile aggregates D(t)
   unsigned long long* inc;  // [ntiles][C][NGA] inclusive prefixes L(t)
   unsigned long long* rec;  // [8][hrec][NW][C][NGS] seed records: per-wave shares of whole-tile sums
+  unsigned* front;          // [8] per run: 1 + the highest run position whose inclusive is published
   void* stats;              // MAVG_AHEAD_STATS builds only: {recomputes, polls that waited}
+  unsigned long long* trace;  // MAVG_CHAIN_TRACE builds only: [ntiles][8] timestamps (chain_trace.py)
   OutParams o;
 };
 
@@ -87,6 +105,50 @@ __device__ __forceinline__ bool link_load(const gran_t* arr, long long j, V (&v)
 template <typename V, int C>
 __device__ __forceinline__ void link_store(gran_t* arr, long long j, const V (&v)[C], int lane) {
   publish_record<V, C>(arr, j, v, lane);
+}
+
+// MAVG_CHAIN_TRACE (tuning builds only, tools/tune/chain_trace.py): per tile,
+// 100-MHz wall-clock stamps of the phases and the look-back's outcome
+#ifdef MAVG_CHAIN_TRACE
+#define MAVG_TRACE(slot, v) (p.trace[(unsigned long long)tile * 8 + (slot)] = (unsigned long long)(v))
+#define MAVG_NOW() __builtin_amdgcn_s_memrealtime()
+#else
+#define MAVG_TRACE(slot, v) ((void)0)
+#define MAVG_NOW() 0ull
+#endif
+
+// A workgroup barrier for LDS hand-offs only: LDS writes drained
+// (lgkmcnt(0)), then s_barrier.  __syncthreads() also drains every global
+// store and atomic (its release fence waits on vmcnt), which would put the
+// chain wave's link stores on the tile waves' critical path.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // gfx9 encoding: lgkmcnt(0), vmcnt/expcnt untouched
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// s_sleep takes an immediate: n units of 64 cycles
+__device__ __forceinline__ void sleep_units(int n) {
+  for (; n > 0; --n) __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ unsigned frontier_load(unsigned* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// L(t-1) from the nearest inclusive L(t-1-ls) (`top`) and the aggregates of
+// lanes ls-1 .. 0 (tiles t-ls .. t-1).  fp64: the strict left fold in
+// increasing tile order, the chain's definition; integers: exact in any order,
+// one wave reduction.
+__device__ __forceinline__ double fold_window(double top, double av, int ls, int lane) {
+  double acc = top;
+#pragma unroll 1
+  for (int l = ls - 1; l >= 0; --l) acc += readlane(av, l);
+  return acc;
+}
+template <typename I>
+__device__ __forceinline__ I fold_window(I top, I av, int ls, int lane) {
+  return top + readlane(wave_incl_scan(lane < ls ? av : (I)0), 63);
 }
 
 __device__ __forceinline__ double readlane_v(double v, int l) { return readlane(v, l); }
@@ -305,14 +367,126 @@ __device__ __forceinline__ void chain_from_seed(const T* __restrict__ in, const 
   }
 }
 
+// The chain wave: after the tile waves' segment totals are in LDS, D(t), the
+// look-back, L(t) and the carry for the tile waves.  A wave of its own, so the
+// look-back's registers never coexist with a tile wave's tile registers (the
+// kernel's VGPR count is the larger of the two paths, not their sum).
+template <typename T, typename A, int C, int F, int U, bool RC>
+__device__ __forceinline__ void chain_wave(const ChainParams& p, const T* __restrict__ in, const T* __restrict__ hist,
+                                           const T* stage, const typename ScanAcc<T, A>::type* tot, A* basep,
+                                           long long tile, long long rs, int run, long long h0, int lane) {
+  using SA = typename ScanAcc<T, A>::type;
+  constexpr int NW = kWG / 64;
+  constexpr int NSEG = U * NW;
+  gran_t* agg = (gran_t*)p.agg;
+  gran_t* inc = (gran_t*)p.inc;
+  // the tile aggregate D(t): the segment totals scanned across lanes in
+  // segment order (the same scan the tile waves use for their prefixes)
+  SA dt[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const SA tv = lane < NSEG ? tot[lane * C + c] : (SA)0;
+    dt[c] = readlane(wave_incl_scan(tv), NSEG - 1);
+  }
+  const long long i = tile - rs;  // position in the run's chain
+  if (lane == 0) MAVG_TRACE(2, MAVG_NOW());
+  A base[C];
+  if (i == 0) {
+    seed_sum<T, A, C, F, U>(in, hist, rs, run, stage, h0, lane, p, base);
+  } else {
+    {
+      A dA[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) dA[c] = (A)dt[c];
+      link_store<A, C>(agg, tile, dA, lane);
+    }
+    // The 64 nearest predecessors' inclusive and aggregate links in one
+    // round of loads: the nearest published inclusive L(t-1-ls), and every
+    // aggregate above it, fold in registers.  No inclusive in the window
+    // (the run's frontier is further back): poll the run's frontier word
+    // -- one load per poll, with backoff, never the whole window (a storm of
+    // window re-reads saturates the XCD's L2) -- until it comes within 64
+    // tiles, then reload the window.  After `spin` rounds without one,
+    // recompute the chain from the run's seed (the same fold, so the same
+    // bits).
+    const long long j = tile - 1 - lane;
+    const bool act = j >= rs && lane < p.reach;
+    const long long jc = act ? j : tile - 1;  // every lane loads (one round for both arrays), inactive ones a valid slot
+    const unsigned need = (unsigned)max(1LL, i + 1 - 64);  // frontier value that puts an inclusive in the window
+#pragma unroll 1
+    for (int it = 0;;) {
+      A iv[C], av[C];
+      const bool hl = link_load<A, C>(inc, jc, iv);
+      const bool al = link_load<A, C>(agg, jc, av);
+      const bool hi = act && hl;
+      bool ha = act && al;
+      const unsigned long long mi = __ballot(hi);
+      if (mi != 0ull) {
+        const int ls = __builtin_ctzll(mi);
+        const unsigned long long below = ls == 0 ? 0ull : ((1ull << ls) - 1ull);
+#pragma unroll 1
+        for (int sp = 0, b = 1; (__ballot(ha) & below) != below && sp < p.spin; ++sp, b = min(2 * b, 32)) {
+#ifdef MAVG_AHEAD_STATS
+          if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats) + 1, 1u);
+#endif
+          sleep_units(b);
+          if (!ha && lane < ls) ha = link_load<A, C>(agg, j, av);
+        }
+        unsigned long long miss = below & ~__ballot(ha);
+#pragma unroll 1
+        while (miss != 0ull) {
+          const int l = __builtin_ctzll(miss);
+          miss &= miss - 1ull;
+          SA dj[C];
+          recompute_aggregate<T, A, C, F, U, RC>(in, hist, tile - 1 - l, lane, p, dj);
+          if (lane == l)
+#pragma unroll
+            for (int c = 0; c < C; ++c) av[c] = (A)dj[c];
+#ifdef MAVG_AHEAD_STATS
+          if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats), 1u);
+#endif
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) base[c] = fold_window(readlane_v(iv[c], ls), av[c], ls, lane);
+        if (lane == 0) MAVG_TRACE(6, (unsigned long long)ls | ((unsigned long long)it << 32));
+        break;
+      }
+      if (p.reach == 0 || it >= p.spin) {
+        chain_from_seed<T, A, C, F, U, RC>(in, hist, rs, run, tile, lane, p, base);
+#ifdef MAVG_AHEAD_STATS
+        if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats), 1u);
+#endif
+        break;
+      }
+#pragma unroll 1
+      for (int b = 1; it < p.spin; b = min(2 * b, 64)) {
+        ++it;
+        sleep_units(b);
+        if (frontier_load(p.front + run) >= need) break;
+      }
+    }
+  }
+  A lt[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) lt[c] = base[c] + (A)dt[c];
+  link_store<A, C>(inc, tile, lt, lane);
+  // advance the run's frontier (monotonic): waiting tiles poll this one word
+  if (lane == 0) {
+    MAVG_TRACE(3, MAVG_NOW());
+    __hip_atomic_fetch_max(p.front + run, (unsigned)(tile - rs + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int c = 0; c < C; ++c) basep[c] = base[c];
+  }
+}
+
 // NT: kNtLoad (tile loads), kNtHalo (shifted-tile loads), kNtStore (outputs).
 // RC: keep the tile's registers across the barriers and rebuild the in-lane
 //     prefix at the output (fewer live fp64 accumulators).
 // DMA: stage interior shifted tiles by LDS-DMA (16-B units).
 // DV: the int16 output division (to_out).
 template <typename T, typename A, int C, int F, int U, int NT, bool RC = false, bool DMA = true, int DV = 0>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(5))) void chain_scan_kernel(ChainParams p) {
-  constexpr int WG = kWG;
+__global__ __launch_bounds__(kWG + 64) void chain_scan_kernel(ChainParams p) {
+  constexpr int WG = kWG;  // tile waves; wave NW (threads WG .. WG+63) is the chain wave
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
   constexpr int TF = WG * F * U;
@@ -328,13 +502,11 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(5))) void c
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* stage = reinterpret_cast<T*>(smem);
   SA* tot = reinterpret_cast<SA*>(smem + kStageBytes);  // [NSEG][C] segment totals
-  A* basep = reinterpret_cast<A*>(tot + NSEG * C);      // [C] the carry L(t-1), from wave 0
+  A* basep = reinterpret_cast<A*>(tot + NSEG * C);      // [C] the carry L(t-1), from the chain wave
 
   const T* __restrict__ in = static_cast<const T*>(p.in);
   T* __restrict__ out = static_cast<T*>(p.out);
   const T* __restrict__ hist = static_cast<const T*>(p.hist);
-  gran_t* agg = (gran_t*)p.agg;
-  gran_t* inc = (gran_t*)p.inc;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = tid >> 6;
@@ -355,6 +527,15 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(5))) void c
   const bool tile_full = (t0 + TF <= nframes);
   MAVG_DCHECK(tile >= 0 && tile < (long long)nb && tile == rs + slot, "chain tile index", tile, slot);
 
+  if (wq == NW) {  // the chain wave: no tile registers
+    __syncthreads();  // A: the shifted stage is complete
+    lds_barrier();    // B: the segment totals are in LDS
+    chain_wave<T, A, C, F, U, RC>(p, in, hist, stage, tot, basep, tile, rs, run, h0, lane);
+    lds_barrier();    // C: the carry is in LDS (the link stores drain on their own)
+    return;
+  }
+
+  if (tid == 0) MAVG_TRACE(0, MAVG_NOW());
   // ---- 1. loads: the tile to registers, the shifted tile to the LDS stage ----
   U_t x[U];
   if (tile_full) {
@@ -412,6 +593,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(5))) void c
   }
   __syncthreads();
 
+  if (tid == 0) MAVG_TRACE(1, MAVG_NOW());
   // ---- 2. d = x - x[n-k]; in-lane, wave and segment scans ----
   auto stage_xk = [&](int j) -> U_t {
     const int e = (Ha + j * F - k) * C;  // stage element of x[n-k]
@@ -460,100 +642,20 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(5))) void c
       if (lane == 0) tot[(u * NW + w) * C + c] = segtot;
     }
   }
-  __syncthreads();
+  lds_barrier();  // B: segment totals in LDS
 
-  // ---- 3. segment prefixes (every wave) and the tile aggregate D(t) ----
+  // ---- 3. segment prefixes (the tile waves) ----
   static_assert(NSEG <= 64, "segment totals are scanned across one wave");
-  SA ex[C], dt[C];
+  SA ex[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const SA tv = lane < NSEG ? tot[lane * C + c] : (SA)0;
-    const SA incl = wave_incl_scan(tv);
-    ex[c] = incl - tv;
-    dt[c] = readlane(incl, NSEG - 1);
+    ex[c] = wave_incl_scan(tv) - tv;
   }
+  lds_barrier();  // C: the chain wave has written the carry
+  if (tid == 0) MAVG_TRACE(4, MAVG_NOW());
 
-  // ---- 4. the chain (wave 0): publish D(t), find L(t-1), publish L(t) ----
-  if (wq == 0) {
-    const long long i = tile - rs;  // position in the run's chain
-    A base[C];
-    if (i == 0) {
-      seed_sum<T, A, C, F, U>(in, hist, rs, run, stage, h0, lane, p, base);
-    } else {
-      {
-        A dA[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) dA[c] = (A)dt[c];
-        link_store<A, C>(agg, tile, dA, lane);
-      }
-      // The 64 nearest predecessors' inclusive and aggregate links in one
-      // round of loads: the nearest published inclusive L(t-1-ls), and every
-      // aggregate above it, fold in registers.  Until one of them publishes
-      // an inclusive, poll (bounded); then recompute the run's chain from its
-      // seed (the pathological path: the same fold, so the same bits).
-      const long long j = tile - 1 - lane;
-      const bool act = j >= rs;
-#pragma unroll 1
-      for (int it = 0;; ++it) {
-        A iv[C], av[C];
-        const bool hi = act && link_load<A, C>(inc, j, iv);
-        bool ha = act && link_load<A, C>(agg, j, av);
-        const unsigned long long mi = __ballot(hi);
-        if (mi != 0ull && __builtin_ctzll(mi) < p.reach) {
-          const int ls = __builtin_ctzll(mi);
-          const unsigned long long below = ls == 0 ? 0ull : ((1ull << ls) - 1ull);
-#pragma unroll 1
-          for (int sp = 0; (__ballot(ha) & below) != below && sp < p.spin; ++sp) {
-#ifdef MAVG_AHEAD_STATS
-            if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats) + 1, 1u);
-#endif
-            __builtin_amdgcn_s_sleep(2);
-            if (!ha && lane < ls) ha = link_load<A, C>(agg, j, av);
-          }
-          unsigned long long miss = below & ~__ballot(ha);
-#pragma unroll 1
-          while (miss != 0ull) {
-            const int l = __builtin_ctzll(miss);
-            miss &= miss - 1ull;
-            SA dj[C];
-            recompute_aggregate<T, A, C, F, U, RC>(in, hist, tile - 1 - l, lane, p, dj);
-            if (lane == l)
-#pragma unroll
-              for (int c = 0; c < C; ++c) av[c] = (A)dj[c];
-#ifdef MAVG_AHEAD_STATS
-            if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats), 1u);
-#endif
-          }
-#pragma unroll
-          for (int c = 0; c < C; ++c) {
-            A acc = readlane_v(iv[c], ls);
-#pragma unroll 1
-            for (int l = ls - 1; l >= 0; --l) acc += readlane_v(av[c], l);
-            base[c] = acc;
-          }
-          break;
-        }
-        if (it >= p.spin) {
-          chain_from_seed<T, A, C, F, U, RC>(in, hist, rs, run, tile, lane, p, base);
-#ifdef MAVG_AHEAD_STATS
-          if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats), 1u);
-#endif
-          break;
-        }
-        __builtin_amdgcn_s_sleep(8);
-      }
-    }
-    A lt[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) lt[c] = base[c] + (A)dt[c];
-    link_store<A, C>(inc, tile, lt, lane);
-    if (lane == 0)
-#pragma unroll
-      for (int c = 0; c < C; ++c) basep[c] = base[c];
-  }
-  __syncthreads();
-
-  // ---- 5. carry + earlier segments; outputs ----
+  // ---- 4. carry + earlier segments; outputs ----
   A w0[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) w0[c] = basep[c];
@@ -592,6 +694,110 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(5))) void c
           for (int c = 0; c < C; ++c) out[(f + fr) * C + c] = y.e[fr * C + c];
     }
   }
+  if (tid == 0) MAVG_TRACE(5, MAVG_NOW());
 }
+
+
+// chained look-back scan (mavg_chain.hpp): zero the link and record
+// granules, then one launch; tile t publishes its aggregate D(t), folds the
+// nearest published inclusive prefix with the aggregates above it, and
+// publishes L(t).
+// Workspace (8-B granules, one block from the start, padded to 16 bytes for
+// the memset's fast form): aggregates and inclusive prefixes, one slot per
+// (tile, channel, 32-bit word of the accumulator), then the run seeds'
+// per-wave records (8 runs x (k/T + 2) tiles x 4 waves), preceded by 64
+// bytes of run frontier words and followed by 16 bytes of launch statistics
+// (MAVG_AHEAD_STATS builds only).
+template <typename T, typename A, int C, int F, int U>
+struct ChainLayout {
+  using SA = typename ScanAcc<T, A>::type;
+  static constexpr int TF = kWG * F * U;
+  long long ntiles, hrec;
+  size_t link_gran, rec_gran;
+  ChainLayout(long long nframes, int k) {
+    ntiles = (nframes + TF - 1) / TF;
+    hrec = (long long)k / TF + 2;
+    link_gran = (size_t)ntiles * C * GranCount<A>::n;
+    rec_gran = (size_t)8 * hrec * kNW * C * GranCount<SA>::n;
+  }
+  // 64 bytes of run frontier words first, then the granules, then 16 bytes of stats
+  size_t bytes() const { return 64 + ((2 * link_gran + rec_gran) * 8 + 15) / 16 * 16 + 16 + trace_bytes(); }
+#ifdef MAVG_CHAIN_TRACE
+  size_t trace_bytes() const { return (size_t)ntiles * 64; }  // tuning builds: 8 stamps per tile, at the end
+#else
+  size_t trace_bytes() const { return 0; }
+#endif
+};
+template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, int DV = 0>
+int launch_chain_scan(const Sig& sg, int k, hipStream_t st, Workspace ws) {
+  const long long nframes = sg.nframes;
+  int reach = 1 << 30, spin = kAheadSpin;
+  {
+    const int t = g_test_ahead_slots.load(std::memory_order_relaxed);
+    if (t >= 0) reach = t;
+    const int s = g_test_ahead_spin.load(std::memory_order_relaxed);
+    if (s >= 0) spin = s;
+  }
+  constexpr int TF = kWG * F * U;
+  constexpr int VE = F * C;
+  constexpr int NSEG = U * kNW;
+  using SA = typename ScanAcc<T, A>::type;
+  constexpr size_t kStageBytes = (((size_t)(U * kWG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15;
+  const ChainLayout<T, A, C, F, U> L(nframes, k);
+  if (L.ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  const size_t need = L.bytes();
+  const size_t lds = kStageBytes + (size_t)NSEG * C * sizeof(SA) + (size_t)C * sizeof(A) + 8;
+  if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text),
+             "chain_scan<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d,rc=%d,dma=%d,dv=%d> grid=%lld block=%d lds=%zu "
+             "tile_frames=%d remap=1 ws=%zu",
+             type_name<T>(), type_name<A>(), C, F, U, NT, (int)RC, (int)DMA, DV, L.ntiles, kWG + 64, lds, TF, need);
+    g_plan->ws_bytes = need;
+    return MAVG_OK;
+  }
+  if (ws.ptr == nullptr || ws.bytes < need) return MAVG_ERR_WORKSPACE;
+  if ((reinterpret_cast<uintptr_t>(ws.ptr) & 15u) != 0) return MAVG_ERR_MISALIGNED;
+  if (hipMemsetAsync(ws.ptr, 0, need, st) != hipSuccess) return MAVG_ERR_HIP;
+  unsigned long long* g = reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(ws.ptr) + 64);
+  ChainParams p{};
+  p.in = sg.in;
+  p.out = sg.out;
+  p.hist = sg.hist;
+  p.nframes = nframes;
+  p.k = k;
+  p.halo_units = (k + F - 1) / F;
+  p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
+  p.hrec = (int)L.hrec;
+  p.spin = spin;
+  p.reach = reach;
+  p.pre = sg.pre;
+  p.eio = sg.eio;
+  p.agg = g;
+  p.inc = g + L.link_gran;
+  p.rec = g + 2 * L.link_gran;
+  p.front = static_cast<unsigned*>(ws.ptr);
+  p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16 - L.trace_bytes();
+  p.trace = reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(ws.ptr) + need - L.trace_bytes());
+  p.o = make_out_params(k);
+  // four tile waves + the chain wave
+  hipLaunchKernelGGL((chain_scan_kernel<T, A, C, F, U, NT, RC, DMA, DV>), dim3((unsigned)L.ntiles), dim3(kWG + 64), lds,
+                     st, p);
+  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+}
+
+// The long-window scan: the chained look-back scan with 4096-frame tiles
+// (U=4 x 16-B units), LDS-DMA shifted stage, non-temporal shifted-tile loads
+// and output stores (its last use), default-policy tile loads (the tile is
+// the shifted tile of tile t + k/T, an L2 hit if it stays); fp32 mono keeps
+// the tile in registers across the barriers (RC).
+template <typename T, typename A, int C, int F>
+int dispatch_long(const Sig& sg, int k, hipStream_t st, Workspace ws) {
+  constexpr int U = 4;
+  constexpr int kNtA = kNtStore | kNtHalo;
+  constexpr bool kRC = sizeof(T) == 4 && C == 1;
+  return launch_chain_scan<T, A, C, F, U, kNtA, kRC, true>(sg, k, st, ws);
+}
+
 
 }  // namespace mavg
