@@ -444,8 +444,6 @@ def run_workload(args, name, rank, world, with_cpu):
                       "the head launch are outside it and only in value / ms_per_step"),
         },
     }
-    if world > 1:
-        line["scaling_detail"] = shard_timing(args, x, y, k, C, algo, ev, hev, value, n, rank, world)
     if args.check:
         res = check_output(y, n, k, C, dt, seed, rank)
         if world > 1:
@@ -455,6 +453,8 @@ def run_workload(args, name, rank, world, with_cpu):
             res = {"ranks": world, "slices": sum(r["slices"] for r in allres),
                    "mismatches": sum(r["mismatches"] for r in allres)}
         line["check"] = res
+    if world > 1:  # after --check: the single launches overwrite the output with a no-halo result
+        line["scaling_detail"] = shard_timing(args, x, y, k, C, algo, ev, hev, value, n, rank, world)
     # same-box streaming ceiling: the library's flat non-temporal copy over the
     # same buffers and step count (after --check: it overwrites the output)
     cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]

@@ -10,7 +10,9 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "lib", "libmavg.so")
+# MAVG_LIBRARY: another build of the same ABI (the debug build,
+# lib/libmavg_debug.so, in tests/test_debug_build.py); default the release build
+LIB_PATH = os.environ.get("MAVG_LIBRARY") or os.path.join(_PKG, "lib", "libmavg.so")
 
 # mavg_dtype
 I16 = 0

@@ -87,6 +87,7 @@ __global__ __launch_bounds__(WG) void direct_kernel(DirectParams p) {
   const long long tile = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
   const long long t0 = tile * TF;
   const long long h0 = t0 - (long long)m * F;
+  MAVG_DCHECK(tile >= 0 && tile < (long long)gridDim.x && t0 < nframes, "direct tile index", tile, gridDim.x);
   const bool tile_full = (t0 + TF <= nframes);
 
   U_t xr[U];
@@ -165,6 +166,7 @@ __global__ __launch_bounds__(WG) void direct_kernel(DirectParams p) {
 #pragma unroll
       for (int c = 0; c < C; ++c) tot[c] = (m >= 2) ? pc[2 * F - 1][c] : pc[F - 1][c];
       for (int j = 2; j < m; ++j) {
+        MAVG_DCHECK(q - m + j >= 0 && q - m + j < m + U * WG, "direct stage unit", q - m + j, m);
         const U_t uj = IO::load(stage + (q - m + j) * VE);
 #pragma unroll
         for (int fr = 0; fr < F; ++fr)

@@ -164,6 +164,7 @@ __device__ __forceinline__ void wave_record(const Unit<T, F * C> (&x)[U], SA (&r
 template <typename SA, int C>
 __device__ __forceinline__ void publish_record(gran_t* gran, long long j, const SA (&r)[C], int lane) {
   constexpr int NG = GranCount<SA>::n;
+  MAVG_DCHECK(j >= 0, "record index", j, lane);
   if (lane < C * NG) {
     const int c = lane / NG, h = lane - c * NG;
     SA v = r[0];
@@ -272,6 +273,7 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
   const long long t0 = tile * TF;
   const int Ha = p.halo_units * F;
   const long long h0 = t0 - Ha;
+  MAVG_DCHECK(tile >= 0 && tile < (long long)gridDim.x && t0 < nframes, "ahead tile index", tile, gridDim.x);
   const bool tile_full = (t0 + TF <= nframes);
   const long long a = t0 - k;                                   // first frame of the window before t0
   const long long jlo = a >= 0 ? (a + TF - 1) / TF : 0;         // first whole tile inside it
@@ -373,6 +375,7 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
   unsigned long long rv[C][NG];
   {
     const long long q = qlo + tid;
+    MAVG_DCHECK(qhi <= p.nfull * RPT, "record read range", qhi, p.nfull);
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -414,9 +417,11 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
     U_t xk;
     if constexpr (IO::kVec) {
       if (p.xk_off == 0) {
+        MAVG_DCHECK(e >= 0 && e + VE <= kStageUnits * VE, "ahead x[n-k] stage index", e, j);
         xk = IO::load(stage + e);
       } else {
         const int e_lo = e - p.xk_off;
+        MAVG_DCHECK(e_lo >= 0 && e_lo + 2 * VE <= kStageUnits * VE, "ahead x[n-k] extraction", e_lo, j);
         U_t a0 = IO::load_whole(stage + e_lo);
         U_t a1 = IO::load_whole(stage + e_lo + VE);
         xk = extract(a0, a1, p.xk_off);

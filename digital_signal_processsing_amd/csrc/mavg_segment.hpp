@@ -61,6 +61,7 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
   const bool eio = F == 1 && p.eio != 0;
 
   const long long seg = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
+  MAVG_DCHECK(seg >= 0 && seg < (long long)gridDim.x && seg * p.seg_frames < nframes, "segment index", seg, gridDim.x);
   const long long s0 = seg * p.seg_frames;
   const long long s1 = min(s0 + p.seg_frames, nframes);
   const long long p0 = s0 - (long long)p.pre_chunks * CHF;
@@ -142,6 +143,7 @@ __global__ __launch_bounds__(kWG) void scan_kernel(ScanParams p) {
       } else if constexpr (IO::kVec) {
         int qk = kb + j * F;
         if (qk >= R) qk -= R;
+        MAVG_DCHECK(qk >= 0 && qk + F <= R, "segment ring x[n-k]", qk, R);
         if (p.xk_off == 0) {
           xk = IO::load(ring + qk * C);
         } else {

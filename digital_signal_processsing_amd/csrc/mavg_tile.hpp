@@ -85,6 +85,9 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
   const long long tile = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
   const long long t0 = tile * TF;
   const long long h0 = t0 - Ha;              // first staged halo frame
+  MAVG_DCHECK(tile >= 0 && tile < p.ntiles && t0 < nframes, "tile index", tile, p.ntiles);
+  MAVG_DCHECK(stage_bytes + (NSEG + NW) * C * (int)sizeof(A) <= (int)(WG >= 1024 ? 80 * 1024 : 64 * 1024),
+              "tile LDS layout", stage_bytes, Hu);
   const bool tile_full = (t0 + TF <= nframes);
 
   constexpr bool kDma = DMA && !HS && IO::kVec && VE * (int)sizeof(T) == 16;
@@ -189,9 +192,11 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
     U_t xk;
     if constexpr (IO::kVec) {
       if (p.xk_off == 0) {
+        MAVG_DCHECK(e >= 0 && e + VE <= (Hu + U * WG + 1) * VE, "tile x[n-k] stage index", e, j);
         xk = IO::load(stage + e);
       } else {
         const int e_lo = e - p.xk_off;
+        MAVG_DCHECK(e_lo >= 0 && e_lo + 2 * VE <= (Hu + U * WG + 1) * VE, "tile x[n-k] extraction", e_lo, j);
         U_t a = IO::load_whole(stage + e_lo);
         U_t b = IO::load_whole(stage + e_lo + VE);
         xk = extract(a, b, p.xk_off);

@@ -276,7 +276,8 @@ def test_gpu_bins_run_the_argv_block_size(tmp_path, stereo_wav, oracle_mod, name
 # hillis_steele_averager.cu:205-207, profilable_parallel_averager.cu:118-121,
 # profilable_sm_averager.cu:141-144), then per memory mode the mode line
 # (e.g. blelloch_scan_averager.cu:237,266) and ProfileResult::print_stats
-# (benchmark.h:47-68; the H2D / D2H lines only when those phases took time).
+# (benchmark.h:47-68; the H2D / D2H lines only when those phases took time),
+# then CsvLogger::log()'s line for the CSV row (gpu_utils.h:230).
 _NUM = r"-?[0-9]+\.[0-9]{3}"
 _STATS = [r"1\. LATENCY BREAKDOWN \(Steady State\)", rf"?   H2D Transfer:   {_NUM} ms",
           rf"   Kernel Compute: {_NUM} ms", rf"?   D2H Transfer:   {_NUM} ms", r"   -----------------------------",
@@ -296,8 +297,9 @@ _HEADERS = {
 def _report_template(name):
     lines = list(_HEADERS.get(name, []))
     for mode in (r"--- MEM MODE: STANDARD \(Discrete\) ---", r"--- MODE: UNIFIED \(Zero-Copy\) ---"):
-        lines += [r"", mode] + _STATS
-    return lines + [r">> Data saved to benchmark_data\.csv"]   # CsvLogger's destructor, gpu_utils.h:230
+        # CsvLogger::log() reports each row it writes (gpu_utils.h:230)
+        lines += [r"", mode] + _STATS + [r">> Data saved to benchmark_data\.csv"]
+    return lines
 
 
 def _match_report(stdout, template):
@@ -332,8 +334,8 @@ def test_gpu_bins_stdout_is_the_reference_report(tmp_path, stereo_wav, name):
 def test_bin_cpu_stdout_is_the_reference_report(tmp_path, stereo_wav):
     """bin_cpu's whole stdout against the reference's CPU averager report:
     header (profilable_moving_averager.cpp:51-53), one stats block (:80),
-    the CSV logger's line (gpu_utils.h:230) -- and the matcher rejects extra
-    lines."""
+    the CSV logger's line (gpu_utils.h:230, printed by log()) -- and the
+    matcher rejects extra lines."""
     path, _ = stereo_wav
     r = _run("bin_cpu", path, 41, 96, cwd=tmp_path)
     assert r.returncode == 0, r.stdout + r.stderr

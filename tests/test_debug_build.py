@@ -1,0 +1,83 @@
+"""The debug build of libmavg (`make -C digital_signal_processsing_amd/csrc debug`
+-> lib/libmavg_debug.so): every kernel family compiled
+with MAVG_DEBUG, whose device checks (MAVG_DCHECK, mavg_device.hpp) guard the
+LDS stage indices, the x[n-k] extractions, the tile / segment indices and the
+record slots, print (check, block, thread, values) and trap.  The GPU test
+runs the golden fixtures and the long-window kernels through it (selected by
+MAVG_LIBRARY in a child process) and checks the outputs against the oracle."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "digital_signal_processsing_amd", "lib")
+DEBUG_LIB = os.path.join(LIB, "libmavg_debug.so")
+CHECK_TEXT = b"mavg debug check failed"
+
+
+def test_debug_library_has_the_checks_and_release_does_not():
+    assert os.path.exists(DEBUG_LIB), "build() makes lib/libmavg_debug.so (make debug)"
+    assert CHECK_TEXT in open(DEBUG_LIB, "rb").read()
+    assert CHECK_TEXT not in open(os.path.join(LIB, "libmavg.so"), "rb").read()
+
+
+def test_debug_library_exports_the_abi():
+    r = subprocess.run([sys.executable, "-c", (
+        "import digital_signal_processsing_amd as d, digital_signal_processsing_amd._lib as l;"
+        "lib = l.load(); print(l.LIB_PATH); print(lib.mavg_abi_version());"
+        "print(all(hasattr(lib, s) for s in l.EXPORTED_SYMBOLS)); print(d.plan(1 << 20, 70000))")],
+        cwd=ROOT, env=dict(os.environ, MAVG_LIBRARY=DEBUG_LIB), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    path, ver, ok, plan = r.stdout.split("\n")[:4]
+    assert path == DEBUG_LIB and ver == "2" and ok == "True" and plan.startswith("ahead_scan<"), r.stdout
+
+
+CHILD = r'''
+import os, numpy as np, torch
+import oracle
+import digital_signal_processsing_amd as dsp
+from digital_signal_processsing_amd import _lib
+oracle.build()
+_lib.load()
+maps = open("/proc/self/maps").read()
+assert "libmavg_debug.so" in maps and "lib/libmavg.so" not in maps, "the debug build must be the one loaded"
+g = np.load(os.path.join("tests", "golden", "mavg_golden.npz"))
+dev = torch.device("cuda:0")
+run = lambda x, k, C, algo, h=None: dsp.moving_average(torch.from_numpy(x).to(dev), k, channels=C, algo=algo,
+                                                      history=None if h is None else torch.from_numpy(h).to(dev)).cpu().numpy()
+algos = ["blelloch", "blelloch_scalar", "hillis", "hillis_scalar", "direct", "direct_vec2", "direct_scalar", "naive"]
+for C in (1, 2):
+    x = oracle.synth_i16(4096 * C, seed=0x5EED)
+    xf = oracle.synth_f32(4096 * C, seed=0x5EED, dist=1)
+    for k in (1, 3, 7, 32, 41, 64, 1000, 1024):
+        for a in algos:
+            assert np.array_equal(run(x, k, C, a), g[f"i16_C{C}_k{k}"]), (a, C, k)
+            y, r = run(xf, k, C, a).astype(np.float64), g[f"f32u_C{C}_k{k}"].astype(np.float64)
+            assert (np.abs(y - r) <= 1e-5 * np.maximum(np.abs(r), 1e-30)).all(), (a, C, k)
+# the look-ahead scan (records, head duty, partial window), int16 with history,
+# the 1024-thread tile, and the segment scan's global x[n-k] path
+xf = oracle.synth_f32(400_003, seed=3, dist=2)
+r = oracle.check_synth_exact(run(xf, 70_000, 1, "blelloch"), 70_000, 1, seed=3, dist=2)
+assert r["mismatches"] == 0, r
+xs = oracle.synth_i16(2 * 150_001, seed=4)
+full = oracle.mavg_i16(xs, 44_100, 2)
+cut = 50_000
+h = xs[(cut - 44_099) * 2: cut * 2]
+assert np.array_equal(run(xs[cut * 2:], 44_100, 2, "blelloch", h), full[cut * 2:])
+assert np.array_equal(run(xs, 12_000, 2, "blelloch"), oracle.mavg_i16(xs, 12_000, 2))
+assert np.array_equal(run(xs, 70_000, 2, "hillis"), oracle.mavg_i16(xs, 70_000, 2))
+torch.cuda.synchronize()
+print("debug build ok")
+'''
+
+
+@pytest.mark.gpu
+def test_debug_build_runs_fixtures_and_long_windows_clean(gpu):
+    """No device check fires (a firing check traps the kernel: the child
+    fails) and every output matches the oracle."""
+    r = subprocess.run([sys.executable, "-u", "-c", CHILD], cwd=ROOT, env=dict(os.environ, MAVG_LIBRARY=DEBUG_LIB),
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "debug build ok" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "mavg debug check failed" not in r.stdout + r.stderr
