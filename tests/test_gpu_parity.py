@@ -281,14 +281,20 @@ def test_many_channels_auto(oracle_mod, gpu):
 
 
 # ---------------------------------------------------------------------------
-# the long-window scan: the look-ahead scan (mavg_lookback.hpp), carry from
-# whole-tile records published inside the launch
-LONG_KERNEL = "ahead_scan"
+# the long-window scans: the row-band scan (mavg_band.hpp: rows of k frames,
+# row-tile sums exchanged inside a band) where its geometry applies, else the
+# look-ahead scan (mavg_lookback.hpp: whole-tile records published inside the
+# launch)
+LONG_KERNELS = ("band_scan", "ahead_scan")
+
+
+def _is_long(plan):
+    return plan.split("<")[0] in LONG_KERNELS
 
 
 def _lookback_tile(dsp, n, k, C, dt):
     plan = dsp.plan(n, k, C, dt)
-    assert plan.startswith(LONG_KERNEL + "<"), plan
+    assert _is_long(plan), plan
     return int(plan.split("tile_frames=")[1].split()[0])
 
 
@@ -303,7 +309,7 @@ def test_ahead_window_edges(oracle_mod, gpu, C, dtype):
     frames = 200_003
     T = _lookback_tile(dsp, frames * C, 70_001, C, dt)
     for k in sorted({16 * T - 1, 16 * T, 16 * T + 1, 20_000, 44_100, 70_001}):
-        if dsp.plan(frames * C, k, C, dt).split("<")[0] != LONG_KERNEL:
+        if not _is_long(dsp.plan(frames * C, k, C, dt)):
             continue
         if dtype == "i16":
             x = oracle_mod.synth_i16(frames * C, offset=k + C)
@@ -373,7 +379,7 @@ def test_ahead_graph_capture(oracle_mod, gpu, own_workspace):
     n, k = 1_000_003, 30_000
     x = torch.from_numpy(oracle_mod.synth_f32(n, seed=23, dist=1)).to(gpu)
     y = torch.empty_like(x)
-    assert dsp.plan(n, k).startswith(LONG_KERNEL + "<")
+    assert _is_long(dsp.plan(n, k))
     ws = torch.empty(dsp.workspace_bytes(n, k), dtype=torch.uint8, device=gpu) if own_workspace else None
     s = torch.cuda.Stream(device=gpu)
     s.wait_stream(torch.cuda.current_stream(gpu))
@@ -447,11 +453,12 @@ def test_ahead_records_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, 
     dt = dsp.F32 if dtype == "f32" else dsp.I16
     frames = 2_600_000 // C + 12_345  # > D = 512 tiles at C=1: the look-ahead producers run
     plan = dsp.plan(frames * C, k, C, dt)
-    assert plan.startswith("ahead_scan<")
-    # mono windows whose per-wave records fit one round of loads take the
-    # per-wave records (wrec=1); the others one record per tile
-    tf = int(plan.split("tile_frames=")[1].split()[0])
-    assert ("wrec=1" in plan) == (C == 1 and k // tf + 1 <= 64), plan
+    assert _is_long(plan), plan
+    if plan.startswith("ahead_scan<"):
+        # mono windows whose per-wave records fit one round of loads take the
+        # per-wave records (wrec=1); the others one record per tile
+        tf = int(plan.split("tile_frames=")[1].split()[0])
+        assert ("wrec=1" in plan) == (C == 1 and k // tf + 1 <= 64), plan
     if dtype == "f32":
         x = oracle_mod.synth_f32(frames * C, seed=77, dist=2)
     else:
