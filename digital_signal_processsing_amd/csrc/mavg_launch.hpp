@@ -239,7 +239,16 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
     const int t = g_test_ahead_spin.load(std::memory_order_relaxed);
     if (t >= 0) spin = t;
   }
-  constexpr int xcd_remap = 1;  // one run per XCD (see ahead_scan_kernel)
+  // one contiguous run per XCD (remap mode 1: x[n-k] is then an L2 hit of the
+  // same XCD) while the window's bytes fit comfortably in an XCD's 4 MB L2;
+  // for longer windows x[n-k] comes from the MALL anyway, and 8 separate runs
+  // would need 8 windows of MALL: runs of 64 tiles per XCD, the 8 XCDs'
+  // runs adjacent, so the chip streams one front (D >= 8 x 64 keeps every
+  // record's producer ahead of its consumers; no head duty).  Measured,
+  // 2^30 fp32: k=4e6 0.185 -> 0.526 of peak, k=1e6 0.524 -> 0.588, int16
+  // stereo k=1e6 0.408 -> 0.509; k=6e5 unchanged (profiles/r03_tuning/remap/)
+  const long long win_bytes = (long long)k * C * (long long)sizeof(T);
+  const int xcd_remap = (win_bytes > (1LL << 21) && ahead >= 8 * 64) ? 64 : 1;
   constexpr int TF = kWG * F * U;
   constexpr int VE = F * C;
   constexpr int NSEG = U * kNW;
@@ -277,7 +286,7 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
   p.xcd_remap = xcd_remap;
   p.ahead = ahead;
-  p.head = (int)std::min<long long>((long long)k / TF, nfull);
+  p.head = xcd_remap == 1 ? (int)std::min<long long>((long long)k / TF, nfull) : 0;  // head duty: mode 1 only
   p.spin = spin;
   p.gran = static_cast<unsigned long long*>(ws.ptr);
   p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
