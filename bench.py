@@ -53,6 +53,11 @@ WORKLOADS = {
     # stereo as its WAV harness writes it)
     "i16_long": (1 << 30, 44100, 1, "i16", "blelloch"),
     "i16_stereo_long": (1 << 30, 44100, 2, "i16", "blelloch"),
+    # the Hillis-Steele flavour past its LDS-staged halo (the look-ahead
+    # record carry with the log-step in-tile scan), and very long windows
+    "hillis_long": (1 << 30, 44100, 1, "f32", "hillis"),
+    "long_1m": (1 << 30, 1_000_000, 1, "f32", "blelloch"),
+    "long_4m": (1 << 30, 4_000_000, 1, "f32", "blelloch"),
 }
 
 

@@ -12,12 +12,10 @@
 //   mavg_tile.hpp      tile_scan_kernel: one short-lived workgroup per flat
 //                      tile; the carry is rebuilt from a k-frame halo staged
 //                      in LDS.  The default for windows up to ~16 KiB of halo.
-//   mavg_segment.hpp   scan_kernel: a workgroup walks a short segment chunk by
-//                      chunk with an LDS ring of the last k frames and a
-//                      k-frame pre-roll (the Hillis-Steele flavour's long windows).
 //   mavg_lookback.hpp  ahead_scan_kernel: one pass over HBM, carry from
-//                      whole-tile records that tiles 64 ahead published
-//                      inside the launch; windows past the LDS-staged halo.
+//                      whole-tile records that tiles D slots ahead published
+//                      inside the launch; windows past the LDS-staged halo,
+//                      both flavours (Blelloch and Hillis-Steele in-tile scans).
 //   mavg_direct.hpp    direct_kernel: small windows summed directly from LDS
 //                      (replaces profilable_sm_*.cu).
 //   mavg_misc.hpp      naive_kernel (profilable_parallel_averager.cu:14-23)
@@ -36,5 +34,4 @@
 #include "mavg_direct.hpp"
 #include "mavg_lookback.hpp"
 #include "mavg_misc.hpp"
-#include "mavg_segment.hpp"
 #include "mavg_tile.hpp"

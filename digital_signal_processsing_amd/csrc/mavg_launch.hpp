@@ -100,66 +100,6 @@ int scan_i16_wide(int C, bool vec, bool hs, const Sig& sg, int k, int block, hip
 int direct_any(int dtype, bool wide, int C, int width, const Sig& sg, int k, int block, hipStream_t st);
 int naive_any(int dtype, bool wide, const Sig& sg, int C, int k, int block, hipStream_t st);
 
-// ---- streaming scan launch ----------------------------------------------------
-// Launch geometry knobs (tuned on MI355X with tools/tune).
-struct ScanTuning {
-  int oversub = 1;          // workgroups per resident slot (1 = one pass of long segments)
-  int min_seg_chunks = 1;   // lower bound on chunks per segment
-  int seg_chunks = 0;       // > 0: fixed segment length in chunks (overrides the two above)
-  int xcd_remap = 0;        // 1: consecutive segments on one XCD
-};
-
-template <typename T, typename A, int C, int F, int U, bool HS, int PD = 1, int NT = 0>
-int launch_scan(const Sig& sg, int k, hipStream_t st, ScanTuning tune = ScanTuning()) {
-  constexpr int CHF = kWG * F * U;
-  constexpr int NSEG = U * kNW;
-  constexpr int VE = F * C;
-  const long long nframes = sg.nframes;
-  ScanParams p{};
-  p.in = sg.in;
-  p.out = sg.out;
-  p.hist = sg.hist;
-  p.nframes = nframes;
-  p.pre = sg.pre;
-  p.eio = sg.eio;
-  p.k = k;
-  p.o = make_out_params(k);
-  p.pre_chunks = (k - 1 + CHF - 1) / CHF;
-  const long long ring_frames = (long long)CHF * (((long long)k + 2LL * CHF + CHF - 1) / CHF);
-  const size_t tot_bytes = 2 * NSEG * C * sizeof(A);
-  size_t ring_bytes = ((size_t)ring_frames * C * sizeof(T) + 15) & ~(size_t)15;
-  p.xkg = 0;
-  if (ring_bytes + tot_bytes > kLdsBudget) {
-    p.xkg = 1;  // very large k: x[n-k] re-read from global memory, 2-chunk x ring
-    ring_bytes = ((size_t)2 * CHF * C * sizeof(T) + 15) & ~(size_t)15;
-    p.ring_frames = 2 * CHF;
-  } else {
-    p.ring_frames = (int)ring_frames;
-  }
-  p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
-  const size_t lds = ring_bytes + tot_bytes;
-
-  // one segment per workgroup; aim for every CU to hold a few workgroups
-  const int wg_per_cu = std::max(1, std::min(8, (int)(160 * 1024 / lds)));
-  const long long target = (long long)device_cu_count() * wg_per_cu * std::max(1, tune.oversub);
-  long long seg = (nframes + target - 1) / target;
-  seg = std::max<long long>((long long)CHF * std::max(1, tune.min_seg_chunks), (seg + CHF - 1) / CHF * CHF);
-  if (tune.seg_chunks > 0) seg = (long long)CHF * tune.seg_chunks;
-  p.seg_frames = seg;
-  p.xcd_remap = tune.xcd_remap;
-  const long long nseg = (nframes + seg - 1) / seg;
-  if (nseg > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
-
-  if (g_plan) {
-    snprintf(g_plan->text, sizeof(g_plan->text),
-             "segment_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,pd=%d,nt=%d,xkg=%d> grid=%lld block=%d lds=%zu",
-             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", PD, NT, p.xkg, nseg, kWG, lds);
-    return MAVG_OK;
-  }
-  hipLaunchKernelGGL((scan_kernel<T, A, C, F, U, HS, PD, NT>), dim3((unsigned)nseg), dim3(kWG), lds, st, p);
-  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
-}
-
 // flat-tile scan: one workgroup per tile, carry rebuilt from the k-frame halo
 // DV: the int16 output division of the tile scan -- the magic multiply, which
 // measured faster than the fp64 product here (int16 stereo k=1024: 0.779 vs
@@ -226,7 +166,7 @@ constexpr size_t ahead_granule_bytes(long long nrec) {
 }
 // ahead: D, the dispatch slots between a record's producer and its tile (a
 // multiple of 8; the test hook overrides it)
-template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0>
+template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0, bool HS = false>
 int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
   const long long nframes = sg.nframes;
   {
@@ -258,14 +198,15 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   const long long nfull = nframes / TF;
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   const size_t need = ahead_granule_bytes<T, A, C, F, U>(nfull * (WREC ? kNW : 1));
-  const size_t lds = kStageBytes + (size_t)kNW * C * sizeof(A) + (size_t)(NSEG + 3 * kNW) * C * sizeof(SA);
+  size_t lds = kStageBytes + (size_t)kNW * C * sizeof(A) + (size_t)(NSEG + 3 * kNW) * C * sizeof(SA);
+  if (HS) lds = (lds + 15) / 16 * 16 + (size_t)U * kWG * VE * sizeof(T);  // + the tile itself (HS)
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,nt=%d,rc=%d,dma=%d,wrec=%d,dv=%d> grid=%lld block=%d lds=%zu "
+             "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dma=%d,wrec=%d,dv=%d> grid=%lld block=%d lds=%zu "
              "tile_frames=%d ahead=%d remap=%d ws=%zu",
-             type_name<T>(), type_name<A>(), C, F, U, NT, (int)RC, (int)DMA, (int)WREC, DV, ntiles, kWG, lds, TF,
-             ahead, xcd_remap, need);
+             type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC, (int)DMA, (int)WREC, DV,
+             ntiles, kWG, lds, TF, ahead, xcd_remap, need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -290,8 +231,8 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.spin = spin;
   p.gran = static_cast<unsigned long long*>(ws.ptr);
   p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
-  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV>), dim3((unsigned)ntiles), dim3(kWG), lds, st,
-                     p);
+  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV, HS>), dim3((unsigned)ntiles), dim3(kWG), lds,
+                     st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
@@ -304,38 +245,17 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
 //     fp32 keeps the tile in registers across the second barrier (RC, fewer
 //     live fp64 accumulators)
 //   otherwise: per-tile records, D = 768 (stereo int16) / 1024
-template <typename T, typename A, int C, int F>
+template <typename T, typename A, int C, int F, bool HS = false>
 int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   constexpr int U = 4;
   constexpr int TF = kWG * F * U;
   constexpr int kNtA = kNtStore | kNtHalo;
-  constexpr bool kRC = sizeof(T) == 4 && C == 1;
+  constexpr bool kRC = sizeof(T) == 4 && C == 1 && !HS;
   if constexpr (C == 1) {
-    if ((long long)k / TF + 1 <= kWG / kNW) return launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true>(sg, k, st, ws, 512);
+    if ((long long)k / TF + 1 <= kWG / kNW)
+      return launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true, 0, HS>(sg, k, st, ws, 512);
   }
-  return launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false>(sg, k, st, ws, C == 2 ? 768 : 1024);
-}
-
-// segment streaming with the launch geometry measured best: short
-// XCD-remapped segments of at least 4 chunks and 4x the pre-roll (5.5-5.7
-// TB/s vs 5.0 for one long segment per workgroup, tools/tune/tune_scan.hip)
-template <typename T, typename A, int C, int F, bool HS>
-int launch_segment_rule(const Sig& sg, int k, hipStream_t st) {
-  constexpr int SU = F >= 4 ? 2 : 8;
-  constexpr int CHF = kWG * F * SU;
-  ScanTuning t;
-  t.xcd_remap = 1;
-  t.seg_chunks = std::max(4, 4 * ((k - 1 + CHF - 1) / CHF));
-  return launch_scan<T, A, C, F, SU, HS, 2, 0>(sg, k, st, t);
-}
-// ... and whether its LDS ring holds the window (else it re-reads x[n-k]
-// from global memory, measured 0.25-0.40 of peak)
-template <typename T, typename A, int C, int F>
-bool segment_ring_fits(int k) {
-  constexpr int SU = F >= 4 ? 2 : 8;
-  constexpr long long CHF = (long long)kWG * F * SU;
-  const long long ring = ((CHF * (((long long)k + 3 * CHF - 1) / CHF) * C * (long long)sizeof(T)) + 15) & ~15LL;
-  return ring + 2LL * SU * kNW * C * (long long)sizeof(A) <= (long long)kLdsBudget;
+  return launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS>(sg, k, st, ws, C == 2 ? 768 : 1024);
 }
 
 // Algorithm selection for the scan family (measured on MI355X with
@@ -351,7 +271,7 @@ bool segment_ring_fits(int k) {
 //     look-ahead scan (dispatch_ahead; needs the workspace)
 //   Hillis-Steele flavour: the halo-staged tile while it fits LDS (fp32: U4 nt
 //   for H <= 512 B, else U8 ntS; int16: U4 x 512 threads ntS), then the
-//   segment-streaming scan.
+//   look-ahead scan with the Hillis-Steele in-tile scan (needs the workspace).
 template <typename T, typename A, int C, int F, bool HS>
 int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace ws) {
   constexpr int VE = F * C;
@@ -440,7 +360,10 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
         return launch_tile_scan<T, A, C, F, 8, HS, kNtS>(sg, k, st, kRemapGroup);
     }
     (void)kB;
-    return launch_segment_rule<T, A, C, F, HS>(sg, k, st);
+    // past the LDS-staged halo: the look-ahead scan's record carry with the
+    // Hillis-Steele in-tile scan (the segment kernel re-read x[n-k] from
+    // global memory beyond its LDS ring: 0.25-0.40 of peak)
+    return dispatch_ahead<T, A, C, F, true>(sg, k, st, ws);
   }
 }
 
@@ -528,7 +451,11 @@ int launch_direct_block(const Sig& sg, int k, int block, hipStream_t st) {
       default: return launch_direct<T, A, C, F, 1, kWG, kNtDirect>(sg, k, st);
     }
   }
+#ifdef MAVG_DIRECT_R1_SHAPE  // tuning builds only: the round-1 shape (one unit per lane, default policy), A/B
+  return launch_direct<T, A, C, F, 1, kWG, 0>(sg, k, st);
+#else
   return launch_direct<T, A, C, F, 2, kWG, kNtDirect>(sg, k, st);
+#endif
 }
 
 // width: 16 (vload4), 8 (vload2) or 0 (one frame per lane); block: the

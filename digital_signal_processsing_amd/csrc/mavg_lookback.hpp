@@ -234,9 +234,14 @@ __device__ __forceinline__ void wave_record_lean(const T* __restrict__ in, long 
 //     wave as soon as its share is summed (no barrier before publication; phase
 //     A's loads are issued first), so records appear earlier in the producer's
 //     life; consumers read NW times as many granules.
+// HS: the Hillis-Steele flavour of the in-tile scan (the tile kernel's HS
+//     form: the tile is also staged in LDS, lane l holds frames l, l+64, ...
+//     of its 64F-frame wave segment, a 6-step DPP log-step scan per register,
+//     O(n log n) work); the record carry is the same.  RC must be off.
 template <typename T, typename A, int C, int F, int U, int NT, bool RC = false, bool DMA = true, bool WREC = false,
-          int DV = 0>
+          int DV = 0, bool HS = false>
 __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
+  static_assert(!(HS && RC), "the Hillis-Steele flavour keeps its per-element prefixes");
   constexpr int WG = kWG;
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
@@ -255,6 +260,9 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
   A* hsum = reinterpret_cast<A*>(smem + kStageBytes);  // [NW][C] carry partials
   SA* tot = reinterpret_cast<SA*>(hsum + NW * C);       // [NSEG][C] segment totals
   SA* shares = tot + NSEG * C;                           // [3][NW][C] wave shares of the records published here
+  // HS: the tile itself, [U*WG] units, after the shares (16-B aligned)
+  T* tstage = reinterpret_cast<T*>(smem + ((kStageBytes + (NW * C * (int)sizeof(A)) +
+                                            (NSEG + 3 * NW) * C * (int)sizeof(SA) + 15) & ~15));
 
   const T* __restrict__ in = static_cast<const T*>(p.in);
   T* __restrict__ out = static_cast<T*>(p.out);
@@ -381,6 +389,10 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
 #pragma unroll
       for (int h = 0; h < NG; ++h) rv[c][h] = q < qhi ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
   }
+  if constexpr (HS) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) IO::store(tstage + (u * WG + tid) * VE, x[u]);
+  }
   __syncthreads();
   // publish the records whose wave shares this block holds: wave src adds
   // source src's NW shares in wave order
@@ -436,6 +448,32 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
   SA lx[U][C];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
+    if constexpr (HS) {
+      // wave segment u: tile frames sb .. sb + 64F - 1, lane l holds sb + r*64 + l
+      const int sb = (u * WG + w * 64) * F;
+      SA run[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) run[c] = (SA)0;
+#pragma unroll
+      for (int r = 0; r < F; ++r) {
+        const int fl = sb + r * 64 + lane;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const T xkv = stage[(Ha + fl - k) * C + c];
+          if (fl < pcount) hp[c] += to_acc<A>(xkv);  // the partial window: x[n-k] of the first pcount frames
+          const SA d = to_acc<SA>(tstage[fl * C + c]) - to_acc<SA>(xkv);
+          const SA incl = wave_incl_scan(d);
+          v[u][r][c] = incl + run[c];
+          run[c] += readlane(incl, 63);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        lx[u][c] = (SA)0;
+        if (lane == 0) tot[(u * NW + w) * C + c] = run[c];
+      }
+      continue;
+    }
     const U_t xk = stage_xk(u * WG + tid);
     const int f0 = (u * WG + tid) * F;
     if (f0 + F <= pcount) {
@@ -574,6 +612,24 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
+    if constexpr (HS) {
+      const long long sb = t0 + (long long)(u * WG + w * 64) * F;
+      A b[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) b[c] = w0[c] + (A)readlane(ex[c], u * NW + wq);
+#pragma unroll
+      for (int r = 0; r < F; ++r) {
+        const long long f = sb + r * 64 + lane;
+        if (tile_full || f < nframes)
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            const T yv = to_out<T, A, DV>(b[c] + (A)v[u][r][c], p.o);
+            if constexpr ((NT & kNtStore) != 0) __builtin_nontemporal_store(yv, out + f * C + c);
+            else out[f * C + c] = yv;
+          }
+      }
+      continue;
+    }
     const long long f = t0 + (long long)(u * WG + tid) * F;
     A b[C];
 #pragma unroll

@@ -117,8 +117,8 @@ def test_plan_describes_launch_without_gpu():
         assert "U=4" in i16(k, c) and "dma=0" in i16(k, c) and "block=256" in i16(k, c), i16(k, c)
     assert "U=2" in i16(64) and "dma=0" in i16(64), i16(64)
     assert dsp.plan(1 << 20, 70_000).startswith("ahead_scan<f32")
-    assert dsp.plan(1 << 20, 70_000, algo="hillis").startswith("segment_scan<") and "xkg=1" in dsp.plan(
-        1 << 20, 70_000, algo="hillis")
+    # Hillis-Steele past its LDS-staged halo: the look-ahead record carry with the HS in-tile scan
+    assert dsp.plan(1 << 20, 70_000, algo="hillis").startswith("ahead_scan<f32,acc=f64,C=1,F=4,U=4,hillis")
     assert dsp.plan(1 << 20, 7, algo="direct").startswith("direct<f32")
     assert dsp.plan(1 << 20, 7, algo="naive").startswith("naive<f32")
     assert "hillis" in dsp.plan(1 << 20, 7, algo="hillis_scalar")
@@ -147,13 +147,14 @@ def test_workspace_only_for_ahead_scan():
     assert dsp.plan(1 << 30, 8192, algo="blelloch_scalar").startswith("ahead_scan<f32,acc=f64,C=1,F=1,U=4")
     assert dsp.workspace_bytes(1 << 30, 8192) == 4 * tiles * 4 * 2 * 8 + 16
     assert dsp.workspace_bytes(1 << 30, 8192, algo="blelloch_scalar") == 4 * tiles * 4 * 2 * 8 + 16
-    assert dsp.plan(1 << 30, 8192, algo="hillis").startswith("segment_scan<")
+    assert dsp.plan(1 << 30, 8192, algo="hillis").startswith("ahead_scan<") and "hillis" in dsp.plan(
+        1 << 30, 8192, algo="hillis")
     # int16 keeps the 1024-thread tile up to ~47 KiB of halo
     assert dsp.workspace_bytes(1 << 30, 8192, dtype=dsp.I16) == 0
     n = 2 * 1_000_003
     st = (n // 2) // 1024     # int16 stereo, frame-unit tiles: one int32 word per (whole tile, channel)
     assert dsp.workspace_bytes(n, 44100, 2, dsp.I16) == (st * 2 * 8 + 15) // 16 * 16 + 16
-    assert dsp.workspace_bytes(1 << 20, 70_000, algo="hillis") == 0
+    assert dsp.workspace_bytes(1 << 20, 70_000, algo="hillis") == dsp.workspace_bytes(1 << 20, 70_000)
     assert dsp.workspace_bytes(0, 70_000) == 0
 
 

@@ -22,6 +22,7 @@ CONFIGS = [
     ("config4_2p30_k4096", 1 << 30, 4096, 1, "f32", "blelloch"),    # configs[3]
     ("long_2p30_k44100", 1 << 30, 44100, 1, "f32", "blelloch"),     # look-ahead scan
     ("hillis_2p30_k1024", 1 << 30, 1024, 1, "f32", "hillis"),
+    ("hillis_2p30_k44100", 1 << 30, 44100, 1, "f32", "hillis"),   # Hillis-Steele through the record carry
     ("i16_2p30_k1024", 1 << 30, 1024, 1, "i16", "blelloch"),
     ("i16_stereo_2p30_k44100", 1 << 30, 44100, 2, "i16", "blelloch"),  # 1 s windows on 44.1 kHz stereo PCM
     ("i16_mono_2p30_k44100", 1 << 30, 44100, 1, "i16", "blelloch"),  # look-ahead scan, int16 mono

@@ -474,6 +474,31 @@ def test_ahead_records_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, 
         assert np.array_equal(base, oracle_mod.mavg_i16(x, k, C))
 
 
+@pytest.mark.parametrize("C,k,dt", [(1, 20_000, "f32"), (1, 70_000, "f32"), (2, 44_100, "i16"), (1, 100_000, "i16"),
+                                    (3, 9_000, "f32")])
+def test_hillis_long_windows_through_the_record_carry(oracle_mod, gpu, C, k, dt):
+    """hillis / hillis_scalar past the LDS-staged halo run the look-ahead
+    scan's record carry with the Hillis-Steele in-tile scan: int16 bit-exact,
+    fp32 rounding data (dist 2) within the bar against the exact sums, and
+    bitwise the same under a forced recompute schedule."""
+    import digital_signal_processsing_amd as dsp
+    import torch
+    frames = 900_007
+    dtc = dsp.F32 if dt == "f32" else dsp.I16
+    for algo in ("hillis", "hillis_scalar"):
+        plan = dsp.plan(frames * C, k, C, dtc, algo)
+        assert plan.startswith("ahead_scan<") and "hillis" in plan, plan
+        if dt == "f32":
+            x = dsp.fill_synthetic(frames * C, torch.float32, seed=31, dist=2, device=gpu)
+        else:
+            x = dsp.fill_synthetic(frames * C, torch.int16, seed=31, device=gpu)
+        y = dsp.moving_average(x, k, channels=C, algo=algo).cpu().numpy()
+        y0 = _with_schedule({"spin": 0, "slots": 0}, lambda: dsp.moving_average(x, k, channels=C, algo=algo).cpu().numpy())
+        assert np.array_equal(y.view(np.uint8), y0.view(np.uint8)), algo
+        r = oracle_mod.check_synth(y, k, C, seed=31, dist=2 if dt == "f32" else 0, rtol=RTOL)
+        assert r["mismatches"] == 0, (algo, r)
+
+
 @pytest.mark.parametrize("fill", [0xFF, "tags"])
 def test_ahead_poisoned_workspace(oracle_mod, gpu, fill):
     """The granules are zeroed on the stream before every launch: a caller

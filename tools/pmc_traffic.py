@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 
 
 TYPE = {"f32": "float", "f64": "double", "i16": "short", "i32": "int", "i64": "long"}
-FAMILY = {"tile_scan": "tile_scan_kernel", "segment_scan": "scan_kernel", "direct": "direct_kernel",
+FAMILY = {"tile_scan": "tile_scan_kernel", "direct": "direct_kernel",
           "naive": "naive_kernel", "ahead_scan": "ahead_scan_kernel"}
 
 
@@ -56,9 +56,7 @@ def plan_key(plan):
         args = (T, acc, kv["C"], kv["F"], kv["U"], wg, kv.get("nt", "0"))
     elif fam == "ahead_scan":
         b = {"0": "false", "1": "true"}
-        args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], b[kv["rc"]], b[kv["dma"]], b[kv["wrec"]], kv["dv"])
-    elif fam == "segment_scan":
-        args = (T, acc, kv["C"], kv["F"], kv["U"], hs, kv["pd"], kv["nt"])
+        args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], b[kv["rc"]], b[kv["dma"]], b[kv["wrec"]], kv["dv"], hs)
     else:
         args = (T, acc)
     return FAMILY[fam], args
