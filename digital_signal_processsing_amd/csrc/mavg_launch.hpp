@@ -245,17 +245,22 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
 //     fp32 keeps the tile in registers across the second barrier (RC, fewer
 //     live fp64 accumulators)
 //   otherwise: per-tile records, D = 768 (stereo int16) / 1024
-template <typename T, typename A, int C, int F, bool HS = false>
+template <typename T, typename A, int C, int F, bool HS = false, int U = 4>
 int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
-  constexpr int U = 4;
   constexpr int TF = kWG * F * U;
   constexpr int kNtA = kNtStore | kNtHalo;
   constexpr bool kRC = sizeof(T) == 4 && C == 1 && !HS;
-  if constexpr (C == 1) {
-    if ((long long)k / TF + 1 <= kWG / kNW)
-      return launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true, 0, HS>(sg, k, st, ws, 512);
+  int s;
+  if (C == 1 && (long long)k / TF + 1 <= kWG / kNW)
+    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true, 0, HS>(sg, k, st, ws, 512);
+  else
+    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS>(sg, k, st, ws, C == 2 ? 768 : 1024);
+  // the Hillis-Steele form also stages the tile: wide frames (e.g. 8 fp32
+  // channels, 32 B) take half tiles to stay inside the LDS budget
+  if constexpr (HS && U > 2) {
+    if (s == MAVG_ERR_UNSUPPORTED) return dispatch_ahead<T, A, C, F, HS, 2>(sg, k, st, ws);
   }
-  return launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS>(sg, k, st, ws, C == 2 ? 768 : 1024);
+  return s;
 }
 
 // Algorithm selection for the scan family (measured on MI355X with

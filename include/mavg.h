@@ -83,9 +83,12 @@ typedef enum {
  * alignment of the views later passed to mavg_run.  0 for every launch
  * except the look-ahead scan that AUTO/BLELLOCH pick for windows too long
  * for an LDS-staged halo (fp32 halos > 16 KiB, e.g. mono k > 4096; int16 past
- * ~47 KiB): 8 B per (whole tile, channel, 32-bit word of the tile sum),
- * padded to 16, + 16, for the smaller tiles of the frame-unit form (16 MiB for
- * 2^30 fp32 mono samples; a misaligned view may run that form).
+ * ~47 KiB): 8-B tagged records, one per (tile, channel, 32-bit word of the
+ * tile sum), or one per (tile, wave, ...) for mono windows short enough for
+ * per-wave records, padded to 16, + 16, sized for the smaller tiles of the
+ * frame-unit form a misaligned view may run (2^30 fp32 mono samples: 64 MiB
+ * at k=8192..44100 with per-wave records, 16 MiB at k=10^6 with per-tile
+ * records; int16 stereo k=44100: 8 MiB).
  * 16-B alignment; contents need no initialisation (mavg_run zeroes them on
  * the stream); one workspace must not serve two launches that may run
  * concurrently. */

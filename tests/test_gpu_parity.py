@@ -684,3 +684,41 @@ def test_explicit_side_stream_long_window(oracle_mod, gpu):
         s.synchronize()
         assert_f32_close(y.cpu().numpy(), oracle_mod.mavg_f32(oracle_mod.synth_f32(n, seed=40 + rep, dist=1), k, 1),
                          f"rep {rep}")
+
+
+DYN_LDS_CHILD = r'''
+import threading, numpy as np, torch
+import oracle
+import digital_signal_processsing_amd as dsp
+oracle.build()
+n, k, C = 2 * 300_007, 10_000, 2
+plan = dsp.plan(n, k, C, dsp.I16)
+assert "block=1024" in plan and int(plan.split("lds=")[1].split()[0]) > 64 * 1024, plan
+x = oracle.synth_i16(n, seed=91)
+ref = oracle.mavg_i16(x, k, C)
+out = {}
+def launch(tag):
+    torch.cuda.set_device(0)  # hipSetDevice re-issued on a thread that has not launched yet
+    y = dsp.moving_average(torch.from_numpy(x).to("cuda:0"), k, channels=C)
+    torch.cuda.synchronize()
+    out[tag] = bool(np.array_equal(y.cpu().numpy(), ref))
+for tag in ("first", "second"):
+    t = threading.Thread(target=launch, args=(tag,))
+    t.start(); t.join()
+assert out == {"first": True, "second": True}, out
+print("dyn lds ok")
+'''
+
+
+def test_dynamic_lds_tile_from_fresh_threads(gpu):
+    """The 1024-thread tile above the default 64 KiB dynamic-LDS limit (int16
+    stereo k=10000, 73 KiB), first launched from a fresh thread after
+    hipSetDevice(0) in a fresh process, then again from another thread: the
+    limit is raised per (kernel, device) on the current device
+    (mavg_launch.hpp raise_dyn_lds_limit), and both outputs match the oracle."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-u", "-c", DYN_LDS_CHILD], cwd=root, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0 and "dyn lds ok" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
