@@ -49,5 +49,13 @@ def test_traffic_json_covers_every_workload():
     t = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
     names = {key.split(":")[0] for key in t}
     assert names == set(bench.WORKLOADS), sorted(set(bench.WORKLOADS) ^ names)
-    for v in t.values():
-        assert 0.99 < v["traffic_over_algorithmic"] < 1.05, v
+    for key, v in t.items():
+        name = key.split(":")[0]
+        n, k, C, dt, algo = bench.WORKLOADS[name]
+        if k * C * (4 if dt == "f32" else 2) > (2 << 20):
+            # windows reaching past what an XCD's 4 MB L2 still holds of the
+            # stream: every x[n-k] is fetched again from beyond L2 (MALL or
+            # HBM): one extra read of the input, ~1.5x (very long windows)
+            assert 1.3 < v["traffic_over_algorithmic"] < 1.55, (key, v)
+        else:
+            assert 0.99 < v["traffic_over_algorithmic"] < 1.05, (key, v)

@@ -54,7 +54,7 @@ def main():
                                  ctypes.c_size_t, ctypes.c_void_p]
         buf = ctypes.create_string_buffer(512)
         lib.mavg_plan.restype = ctypes.c_int
-        lib.mavg_plan(ctypes.c_size_t(n), a.c, a.k, code, 0, a.blocks[li], buf, ctypes.c_size_t(512))
+        lib.mavg_plan(ctypes.c_size_t(n), a.c, a.k, code, a.algo, a.blocks[li], buf, ctypes.c_size_t(512))
         p = f"{p} block={a.blocks[li]}"
         libs.append((p, lib, buf.value.decode()))
         blocks[p] = a.blocks[li]
