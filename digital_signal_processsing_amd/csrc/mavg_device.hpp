@@ -287,20 +287,29 @@ __device__ __forceinline__ T load_elem(const T* __restrict__ in, const T* __rest
 // 5.5 T1).  32-bit scalar arithmetic only (the grid is < 2^31 workgroups):
 // a 64-bit divide here costs ~150 SALU instructions per wave.
 // mode 0: identity; 1: each XCD takes one contiguous run of nb/8 tiles
-// (bijective for any nb); G = 2^g > 1: each XCD takes runs of G consecutive
-// tiles and the 8 XCDs' runs are adjacent, so the whole chip works inside a
-// window of 8G tiles; blocks past the last full group of 8G map to themselves.
+// (bijective for any nb); G > 1: each XCD takes runs of G consecutive tiles
+// and the 8 XCDs' runs are adjacent (a "period" of 8G tiles), so the whole
+// chip works inside a window of 8G tiles and tile t + 8G runs on t's XCD;
+// blocks past the last full period map to themselves.  G a power of two:
+// shifts; otherwise one 32-bit divide per call.
 __device__ __forceinline__ long long remap_tile(unsigned b, unsigned nb, int mode) {
   if (mode == 0) return b;
   if (mode == 1) {
     const unsigned q = nb >> 3, r = nb & 7u, x = b & 7u;
     return (long long)((x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3));
   }
-  const unsigned g = (unsigned)__builtin_ctz((unsigned)mode);  // mode = G, a power of two
-  const unsigned full = nb & ~((8u << g) - 1u);
-  if (b >= full) return b;
+  const unsigned G = (unsigned)mode;
   const unsigned i = b >> 3, x = b & 7u;
-  return (long long)(((i >> g) << (g + 3)) + (x << g) + (i & ((1u << g) - 1u)));
+  if ((G & (G - 1u)) == 0u) {
+    const unsigned g = (unsigned)__builtin_ctz(G);
+    const unsigned full = nb & ~((8u << g) - 1u);
+    if (b >= full) return b;
+    return (long long)(((i >> g) << (g + 3)) + (x << g) + (i & (G - 1u)));
+  }
+  const unsigned full = nb - nb % (8u * G);
+  if (b >= full) return b;
+  const unsigned per = i / G;
+  return (long long)(per * 8u * G + x * G + (i - per * G));
 }
 
 // One 16-B LDS-DMA load per lane (global_load_lds_dwordx4): lane l's 16 bytes

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -164,6 +165,22 @@ constexpr size_t ahead_granule_bytes(long long nrec) {
   // + 16 bytes of launch statistics (MAVG_AHEAD_STATS builds only)
   return (((size_t)(nrec > 0 ? nrec : 1) * C * GranCount<SA>::n * 8) + 15) / 16 * 16 + 16;
 }
+// Windows past an XCD's L2 reach (ahead_scan_kernel): window-matched runs
+// (period_tile, kRemapPeriod).  J, the periods per window, is the smallest
+// that keeps the average run g = k / (8 J T) <= D/32 tiles: a record is needed
+// at most ceil(g) - 1 slots before its tile's own dispatch slot, and its
+// producer runs D/8 slots ahead of that tile, so most of the look-ahead stays as
+// margin.  An XCD's L2 then holds the last k/8 frames it read (J periods).
+#ifndef MAVG_AHEAD_PERIOD_MAX_DIV
+#define MAVG_AHEAD_PERIOD_MAX_DIV 32
+#endif
+inline int ahead_periods(long long k, int TF, int ahead) {
+  const double gmax = std::max(2, ahead / MAVG_AHEAD_PERIOD_MAX_DIV);
+  int J = 1;
+  while ((double)k / (8.0 * J * TF) > gmax) ++J;
+  return J;
+}
+
 // ahead: D, the dispatch slots between a record's producer and its tile (a
 // multiple of 8; the test hook overrides it)
 template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0, bool HS = false>
@@ -187,9 +204,17 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   // record's producer ahead of its consumers; no head duty).  Measured,
   // 2^30 fp32: k=4e6 0.185 -> 0.526 of peak, k=1e6 0.524 -> 0.588, int16
   // stereo k=1e6 0.408 -> 0.509; k=6e5 unchanged (profiles/r03_tuning/remap/)
-  const long long win_bytes = (long long)k * C * (long long)sizeof(T);
-  const int xcd_remap = (win_bytes > (1LL << 21) && ahead >= 8 * 64) ? 64 : 1;
   constexpr int TF = kWG * F * U;
+  const long long win_bytes = (long long)k * C * (long long)sizeof(T);
+#ifdef MAVG_AHEAD_FIXED_RUN
+  const int xcd_remap = win_bytes > (1LL << 21) ? MAVG_AHEAD_FIXED_RUN : 1;
+#else
+  const int xcd_remap = win_bytes > (1LL << 21) && (long long)k >= 8LL * TF ? kRemapPeriod : 1;
+#endif
+#ifdef MAVG_AHEAD_PERIOD_D  // tuning builds: the look-ahead distance of window-matched runs
+  if (xcd_remap == kRemapPeriod && g_test_ahead_slots.load(std::memory_order_relaxed) < 0) ahead = MAVG_AHEAD_PERIOD_D;
+#endif
+  const int J = xcd_remap == kRemapPeriod ? ahead_periods(k, TF, ahead) : 0;
   constexpr int VE = F * C;
   constexpr int NSEG = U * kNW;
   using SA = typename ScanAcc<T, A>::type;
@@ -204,9 +229,9 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
              "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dma=%d,wrec=%d,dv=%d> grid=%lld block=%d lds=%zu "
-             "tile_frames=%d ahead=%d remap=%d ws=%zu",
+             "tile_frames=%d ahead=%d remap=%s%d ws=%zu",
              type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC, (int)DMA, (int)WREC, DV,
-             ntiles, kWG, lds, TF, ahead, xcd_remap, need);
+             ntiles, kWG, lds, TF, ahead, J ? "period" : "", J ? J : xcd_remap, need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -226,6 +251,12 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.halo_units = (k + F - 1) / F;
   p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
   p.xcd_remap = xcd_remap;
+  if (J > 0) {  // window-matched runs: pfull = 8 S(P), P the last complete period
+    p.pden = 8LL * J * TF;
+    const long long q = ntiles / 8;
+    const long long P = ((q + 1) * p.pden - 1) / k;
+    p.pfull = (unsigned)(8 * (P * (long long)k / p.pden));
+  }
   p.ahead = ahead;
   p.head = xcd_remap == 1 ? (int)std::min<long long>((long long)k / TF, nfull) : 0;  // head duty: mode 1 only
   p.spin = spin;

@@ -181,6 +181,24 @@ __device__ __forceinline__ long long run_start(unsigned x, unsigned nb) {
   return (long long)(x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q);
 }
 
+// Window-matched runs (launch_ahead_scan, windows past an XCD's L2 reach):
+// period p holds 8 adjacent runs, one per XCD, of G_p = S(p+1) - S(p) tiles,
+// S(p) = floor(p k / pden), pden = 8 J T.  The periods average k / (J T)
+// tiles exactly, so x[n-k]'s tile, k/T tiles back, lies J periods back at the
+// same place of a run of t's own XCD (read J * G of its dispatch slots
+// earlier: an L2 hit), whatever k; the chip streams one front of 8 runs.
+// Blocks from `pfull` (the complete periods) on map to themselves.  64-bit
+// divides: once per tile mapping, for windows of >= 2 MB only.
+constexpr int kRemapPeriod = -1;
+__device__ __forceinline__ long long period_tile(unsigned b, unsigned long long k, unsigned long long pden,
+                                                 unsigned pfull) {
+  if (b >= pfull) return b;
+  const unsigned long long i = b >> 3, x = b & 7u;
+  const unsigned long long per = ((i + 1) * pden - 1) / k;
+  const unsigned long long s0 = per * k / pden, s1 = (per + 1) * k / pden;
+  return (long long)(8 * s0 + x * (s1 - s0) + (i - s0));
+}
+
 struct AheadParams {
   const void* in;
   void* out;
@@ -190,7 +208,9 @@ struct AheadParams {
   int k;
   int halo_units;   // ceil(k / F): the stage starts halo_units*F frames before the tile
   int xk_off;       // (-k*C) mod VE
-  int xcd_remap;    // remap mode (remap_tile)
+  int xcd_remap;    // remap mode (remap_tile), or kRemapPeriod (period_tile)
+  unsigned pfull;   // kRemapPeriod: blocks of the complete periods
+  long long pden;   // kRemapPeriod: 8 J T
   int ahead;        // D (a multiple of 8): block b publishes the records of block b + D's tile
   int head;         // whole tiles a window can span (k / T): the head duty of remap mode 1
   int spin;         // polls of an untagged granule before recomputing it
@@ -277,7 +297,11 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
   const int pre = p.pre;
   const bool eio = F == 1 && p.eio != 0;
 
-  const long long tile = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
+  auto map_tile = [&](unsigned b) -> long long {
+    return p.xcd_remap == kRemapPeriod ? period_tile(b, (unsigned long long)p.k, (unsigned long long)p.pden, p.pfull)
+                                       : remap_tile(b, gridDim.x, p.xcd_remap);
+  };
+  const long long tile = map_tile(blockIdx.x);
   const long long t0 = tile * TF;
   const int Ha = p.halo_units * F;
   const long long h0 = t0 - Ha;
@@ -294,7 +318,7 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
   //         (as late as possible: a record read early may not be published yet) ----
   const unsigned nb = gridDim.x;
   const unsigned bd = blockIdx.x + (unsigned)p.ahead;  // the block D dispatch slots later (same XCD)
-  const long long ja = bd < nb ? remap_tile(bd, nb, p.xcd_remap) : -1;
+  const long long ja = bd < nb ? map_tile(bd) : -1;
   const bool produce = ja >= 0 && ja < p.nfull;
   U_t xa[U];
   if constexpr (WREC) {  // phase A's loads first: the HBM fetch with the longest latency

@@ -269,6 +269,30 @@ def test_grouped_xcd_remap_with_tail(oracle_mod, gpu, dtype, C, k):
         assert np.array_equal(_run(x, k, C, "auto", gpu), oracle_mod.mavg_i16(x, k, C)), plan
 
 
+@pytest.mark.parametrize("dtype,C,k", [("f32", 1, 600_000), ("i16", 2, 1_000_000), ("f32", 1, 4_000_000)])
+def test_period_remap_very_long_windows_with_tail(oracle_mod, gpu, dtype, C, k):
+    """Windows past the L2 reach: the look-ahead scan runs in window-matched
+    runs (period_tile: J periods of 8 runs per window, run lengths floor/ceil
+    of k/(8JT)); two periods and a ragged tail past them (blocks mapped to
+    themselves), every output against the oracle."""
+    import digital_signal_processsing_amd as dsp
+    code = dsp.F32 if dtype == "f32" else dsp.I16
+    plan = dsp.plan(1 << 30, k, C, code)
+    remap = plan.split("remap=")[1].split()[0]
+    tile = int(plan.split("tile_frames=")[1].split()[0])
+    assert plan.startswith("ahead_scan<") and remap.startswith("period"), plan
+    J = int(remap[len("period"):])
+    frames = int(tile * (2 * k / (tile * J) + 37)) + 5  # two periods of k/J frames and a ragged tail
+    assert dsp.plan(frames * C, k, C, code).split("remap=")[1].split()[0] == remap
+    if dtype == "f32":
+        x = oracle_mod.synth_f32(frames * C, dist=2)  # offset 0: the checker's stream starts at the signal's start
+        r = oracle_mod.check_synth_exact(_run(x, k, C, "auto", gpu), k, C, dist=2)
+        assert r["mismatches"] == 0, (plan, r)
+    else:
+        x = oracle_mod.synth_i16(frames * C, offset=77)
+        assert np.array_equal(_run(x, k, C, "auto", gpu), oracle_mod.mavg_i16(x, k, C)), plan
+
+
 def test_many_channels_auto(oracle_mod, gpu):
     """C > 8 (beyond the templated kernels): AUTO runs the naive any-C kernel."""
     for C, dtype in ((12, "i16"), (16, "f32")):

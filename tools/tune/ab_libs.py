@@ -24,7 +24,7 @@ import digital_signal_processsing_amd as dsp
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("libs", nargs=2)
+    ap.add_argument("libs", nargs="+", help="two or more library builds")
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--c", type=int, default=1)
     ap.add_argument("--dtype", default="i16", choices=["i16", "f32"])
@@ -34,9 +34,11 @@ def main():
     ap.add_argument("--dist", type=int, default=0, help="synthetic distribution (fp32: 0, 1, 2)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--ypad", type=int, default=0, help="offset y by this many bytes inside a bigger buffer")
-    ap.add_argument("--blocks", type=int, nargs=2, default=[0, 0],
+    ap.add_argument("--blocks", type=int, nargs="+", default=None,
                     help="block_size per library (0: the tuned dispatch; else the reference's block size)")
     a = ap.parse_args()
+    a.blocks = a.blocks or [0] * len(a.libs)
+    assert len(a.libs) >= 2 and len(a.blocks) == len(a.libs)
     n = 1 << a.log2n
     tdt = torch.int16 if a.dtype == "i16" else torch.float32
     code = dsp.I16 if a.dtype == "i16" else dsp.F32
@@ -107,7 +109,8 @@ def main():
     byt = 2 * x.element_size() * n
     print(f"n=2^{a.log2n} k={a.k} C={a.c} dtype={a.dtype} rounds={a.rounds} steps={a.steps} "
           f"y-x={y.data_ptr() - x.data_ptr():#x}  outputs equal: "
-          f"{bool(torch.equal(outs[0], outs[1]))}  max |diff| {float((outs[0].double() - outs[1].double()).abs().max()):.3g}")
+          f"{all(bool(torch.equal(outs[0], o)) for o in outs[1:])}  max |diff| "
+          f"{max(float((outs[0].double() - o.double()).abs().max()) for o in outs[1:]):.3g}")
     for p, lib, plan in libs + [("torch copy_", None, "")]:
         t = times[p]
         mean, med = statistics.mean(t), statistics.median(t)
