@@ -167,15 +167,16 @@ constexpr size_t ahead_granule_bytes(long long nrec) {
 }
 // Windows past an XCD's L2 reach (ahead_scan_kernel): window-matched runs
 // (period_tile, kRemapPeriod).  J, the periods per window, is the smallest
-// that keeps the average run g = k / (8 J T) <= D/32 tiles: a record is needed
-// at most ceil(g) - 1 slots before its tile's own dispatch slot, and its
-// producer runs D/8 slots ahead of that tile, so most of the look-ahead stays as
-// margin.  An XCD's L2 then holds the last k/8 frames it read (J periods).
-#ifndef MAVG_AHEAD_PERIOD_MAX_DIV
-#define MAVG_AHEAD_PERIOD_MAX_DIV 32
+// that keeps the average run g = k / (8 J T) <= min(32, D/16) tiles: a record
+// is needed at most ceil(g) - 1 slots before its tile's own dispatch slot,
+// and its producer runs D/8 slots ahead of that tile, so most of the
+// look-ahead stays as margin; short runs also keep each XCD's share of the
+// front small.  An XCD's L2 then holds the last k/8 frames it read (J periods).
+#ifndef MAVG_AHEAD_RUN_MAX
+#define MAVG_AHEAD_RUN_MAX 32
 #endif
 inline int ahead_periods(long long k, int TF, int ahead) {
-  const double gmax = std::max(2, ahead / MAVG_AHEAD_PERIOD_MAX_DIV);
+  const double gmax = std::max(2, std::min(MAVG_AHEAD_RUN_MAX, ahead / 16));
   int J = 1;
   while ((double)k / (8.0 * J * TF) > gmax) ++J;
   return J;
