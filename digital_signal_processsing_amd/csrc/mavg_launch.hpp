@@ -165,26 +165,40 @@ constexpr size_t ahead_granule_bytes(long long nrec) {
   // + 16 bytes of launch statistics (MAVG_AHEAD_STATS builds only)
   return (((size_t)(nrec > 0 ? nrec : 1) * C * GranCount<SA>::n * 8) + 15) / 16 * 16 + 16;
 }
-// Windows past an XCD's L2 reach (ahead_scan_kernel): window-matched runs
-// (period_tile, kRemapPeriod).  J, the periods per window, is the smallest
-// that keeps the average run g = k / (8 J T) <= min(32, D/16) tiles: a record
-// is needed at most ceil(g) - 1 slots before its tile's own dispatch slot,
-// and its producer runs D/8 slots ahead of that tile, so most of the
-// look-ahead stays as margin; short runs also keep each XCD's share of the
-// front small.  An XCD's L2 then holds the last k/8 frames it read (J periods).
+// Windows past an XCD's L2 reach (ahead_scan_kernel): window-matched runs,
+// remap mode G.  The window is m = k/T tiles; with runs of G tiles a period
+// is 8G, and x[n-k]'s tile lies J periods back on the tile's own XCD when
+// 8JG ~ m, off by d = |m - 8JG| tiles: a fraction ~d/G of the tiles reads it
+// from another XCD.  G <= min(48, D/20) keeps each record's producer (D/8
+// slots ahead of its tile) and each run total's (D/8 - 2G) ahead of their
+// consumers; among the J that allow it (up to 8 more than the smallest) the
+// one with the smallest d/G wins.
 #ifndef MAVG_AHEAD_RUN_MAX
-#define MAVG_AHEAD_RUN_MAX 32
+#define MAVG_AHEAD_RUN_MAX 48
 #endif
-inline int ahead_periods(long long k, int TF, int ahead) {
-  const double gmax = std::max(2, std::min(MAVG_AHEAD_RUN_MAX, ahead / 16));
+inline int ahead_run_length(long long k, int TF, int ahead) {
+  const int gmax = std::max(2, std::min(MAVG_AHEAD_RUN_MAX, ahead / 20));
+  const double m = (double)k / TF;
   int J = 1;
-  while ((double)k / (8.0 * J * TF) > gmax) ++J;
-  return J;
+  while (m / (8.0 * J) > gmax + 0.5) ++J;
+  int best = 0;
+  double best_miss = 2.0;
+  for (int j = J; j < J + 8; ++j) {
+    const int G = std::max(2, (int)std::lround(m / (8.0 * j)));
+    const double miss = std::fabs(m - 8.0 * j * G) / G;
+    if (G <= gmax && miss < best_miss - 1e-9) best_miss = miss, best = G;
+  }
+  return best > 0 ? best : gmax;
 }
 
 // ahead: D, the dispatch slots between a record's producer and its tile (a
 // multiple of 8; the test hook overrides it)
-template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0, bool HS = false>
+// Windows past an XCD's L2 reach run in window-matched runs (remap mode G)
+inline bool ahead_past_l2(long long k, int C, int elem, int TF) {
+  return k * C * elem > (1LL << 21) && k >= 8LL * TF;
+}
+template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0, bool HS = false,
+          bool RUNS = false>
 int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
   const long long nframes = sg.nframes;
   {
@@ -199,23 +213,19 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   }
   // one contiguous run per XCD (remap mode 1: x[n-k] is then an L2 hit of the
   // same XCD) while the window's bytes fit comfortably in an XCD's 4 MB L2;
-  // for longer windows x[n-k] comes from the MALL anyway, and 8 separate runs
-  // would need 8 windows of MALL: runs of 64 tiles per XCD, the 8 XCDs'
-  // runs adjacent, so the chip streams one front (D >= 8 x 64 keeps every
-  // record's producer ahead of its consumers; no head duty).  Measured,
-  // 2^30 fp32: k=4e6 0.185 -> 0.526 of peak, k=1e6 0.524 -> 0.588, int16
-  // stereo k=1e6 0.408 -> 0.509; k=6e5 unchanged (profiles/r03_tuning/remap/)
+  // past that, 8 separate runs would fetch x[n-k] from the MALL: window-
+  // matched runs (ahead_run_length), the chip streaming one front, no head duty.
+  // Measured, 2^30 fp32 (profiles/r03_tuning/remap/, period/): one run per
+  // XCD -> runs of 64 tiles -> window-matched runs: k=4e6 0.185 -> 0.526;
+  // k=1e6 0.524 -> 0.588 -> 0.668; k=6e5 0.594 -> 0.599 -> 0.681
   constexpr int TF = kWG * F * U;
-  const long long win_bytes = (long long)k * C * (long long)sizeof(T);
 #ifdef MAVG_AHEAD_FIXED_RUN
-  const int xcd_remap = win_bytes > (1LL << 21) ? MAVG_AHEAD_FIXED_RUN : 1;
+  const int xcd_remap = ahead_past_l2(k, C, sizeof(T), TF) ? MAVG_AHEAD_FIXED_RUN : 1;
+  static_assert(!RUNS, "run totals need window-matched runs");
 #else
-  const int xcd_remap = win_bytes > (1LL << 21) && (long long)k >= 8LL * TF ? kRemapPeriod : 1;
+  const int xcd_remap = ahead_past_l2(k, C, sizeof(T), TF) ? ahead_run_length(k, TF, ahead) : 1;
+  if (RUNS && xcd_remap == 1) return MAVG_ERR_UNSUPPORTED;
 #endif
-#ifdef MAVG_AHEAD_PERIOD_D  // tuning builds: the look-ahead distance of window-matched runs
-  if (xcd_remap == kRemapPeriod && g_test_ahead_slots.load(std::memory_order_relaxed) < 0) ahead = MAVG_AHEAD_PERIOD_D;
-#endif
-  const int J = xcd_remap == kRemapPeriod ? ahead_periods(k, TF, ahead) : 0;
   constexpr int VE = F * C;
   constexpr int NSEG = U * kNW;
   using SA = typename ScanAcc<T, A>::type;
@@ -223,16 +233,24 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   const long long ntiles = (nframes + TF - 1) / TF;
   const long long nfull = nframes / TF;
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
-  const size_t need = ahead_granule_bytes<T, A, C, F, U>(nfull * (WREC ? kNW : 1));
+  // runs with a published total: run r's is published with the record of
+  // the last tile of run r + 8, which must be a whole tile of a complete
+  // period (remap_tile maps the blocks past those to themselves)
+  const long long P = xcd_remap > 1 ? ntiles / (8LL * xcd_remap) : 0;
+  const long long pub_periods = P - 1 - (8LL * xcd_remap * P > nfull ? 1 : 0);
+  const long long runs_done = RUNS && pub_periods > 0 ? 8 * pub_periods : 0;
+  const size_t rec_bytes = ahead_granule_bytes<T, A, C, F, U>(nfull * (WREC ? kNW : 1)) - 16;
+  const size_t run_bytes = ((size_t)runs_done * C * GranCount<A>::n * 8 + 15) / 16 * 16;
+  const size_t need = rec_bytes + run_bytes + 16;
   size_t lds = kStageBytes + (size_t)kNW * C * sizeof(A) + (size_t)(NSEG + 3 * kNW) * C * sizeof(SA);
   if (HS) lds = (lds + 15) / 16 * 16 + (size_t)U * kWG * VE * sizeof(T);  // + the tile itself (HS)
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
              "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dma=%d,wrec=%d,dv=%d> grid=%lld block=%d lds=%zu "
-             "tile_frames=%d ahead=%d remap=%s%d ws=%zu",
+             "tile_frames=%d ahead=%d remap=%d%s ws=%zu",
              type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC, (int)DMA, (int)WREC, DV,
-             ntiles, kWG, lds, TF, ahead, J ? "period" : "", J ? J : xcd_remap, need);
+             ntiles, kWG, lds, TF, ahead, xcd_remap, RUNS ? " runs=1" : "", need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -252,19 +270,15 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.halo_units = (k + F - 1) / F;
   p.xk_off = (int)((VE - ((long long)k * C) % VE) % VE);
   p.xcd_remap = xcd_remap;
-  if (J > 0) {  // window-matched runs: pfull = 8 S(P), P the last complete period
-    p.pden = 8LL * J * TF;
-    const long long q = ntiles / 8;
-    const long long P = ((q + 1) * p.pden - 1) / k;
-    p.pfull = (unsigned)(8 * (P * (long long)k / p.pden));
-  }
+  p.runs_done = runs_done;
   p.ahead = ahead;
   p.head = xcd_remap == 1 ? (int)std::min<long long>((long long)k / TF, nfull) : 0;  // head duty: mode 1 only
   p.spin = spin;
   p.gran = static_cast<unsigned long long*>(ws.ptr);
+  p.runs = reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(ws.ptr) + rec_bytes);
   p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
-  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV, HS>), dim3((unsigned)ntiles), dim3(kWG), lds,
-                     st, p);
+  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV, HS, RUNS>), dim3((unsigned)ntiles),
+                     dim3(kWG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
@@ -282,11 +296,20 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   constexpr int TF = kWG * F * U;
   constexpr int kNtA = kNtStore | kNtHalo;
   constexpr bool kRC = sizeof(T) == 4 && C == 1 && !HS;
+  constexpr int D = C == 2 ? 768 : 1024;
   int s;
   if (C == 1 && (long long)k / TF + 1 <= kWG / kNW)
     s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true, 0, HS>(sg, k, st, ws, 512);
+#if !defined(MAVG_AHEAD_FIXED_RUN) && !defined(MAVG_AHEAD_NO_RUNS)
+  // run totals (O(J + G) carry items instead of k/T) where the windows are
+  // long enough to pay for the kernel's extra registers (4 waves per SIMD
+  // instead of 5): > 384 tiles (A/B, profiles/r03_tuning/runs/: fp32
+  // k=4e6 0.543 -> 0.596, k=2e6 0.623 -> 0.641; k=1e6 0.670 -> 0.642)
+  else if (C <= 2 && U == 4 && !HS && ahead_past_l2(k, C, sizeof(T), TF) && (long long)k > 384LL * TF)
+    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS, C <= 2 && U == 4 && !HS>(sg, k, st, ws, D);
+#endif
   else
-    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS>(sg, k, st, ws, C == 2 ? 768 : 1024);
+    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS>(sg, k, st, ws, D);
   // the Hillis-Steele form also stages the tile: wide frames (e.g. 8 fp32
   // channels, 32 B) take half tiles to stay inside the LDS budget
   if constexpr (HS && U > 2) {

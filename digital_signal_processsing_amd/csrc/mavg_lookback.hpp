@@ -182,21 +182,17 @@ __device__ __forceinline__ long long run_start(unsigned x, unsigned nb) {
 }
 
 // Window-matched runs (launch_ahead_scan, windows past an XCD's L2 reach):
-// period p holds 8 adjacent runs, one per XCD, of G_p = S(p+1) - S(p) tiles,
-// S(p) = floor(p k / pden), pden = 8 J T.  The periods average k / (J T)
-// tiles exactly, so x[n-k]'s tile, k/T tiles back, lies J periods back at the
-// same place of a run of t's own XCD (read J * G of its dispatch slots
-// earlier: an L2 hit), whatever k; the chip streams one front of 8 runs.
-// Blocks from `pfull` (the complete periods) on map to themselves.  64-bit
-// divides: once per tile mapping, for windows of >= 2 MB only.
-constexpr int kRemapPeriod = -1;
-__device__ __forceinline__ long long period_tile(unsigned b, unsigned long long k, unsigned long long pden,
-                                                 unsigned pfull) {
-  if (b >= pfull) return b;
-  const unsigned long long i = b >> 3, x = b & 7u;
-  const unsigned long long per = ((i + 1) * pden - 1) / k;
-  const unsigned long long s0 = per * k / pden, s1 = (per + 1) * k / pden;
-  return (long long)(8 * s0 + x * (s1 - s0) + (i - s0));
+// remap_tile mode G: runs of G consecutive tiles, run r = tiles [rG, rG + G)
+// on XCD r mod 8, 8 adjacent runs per period; G ~ k / (8 J T) so that x[n-k]'s
+// tile, k/T tiles back, lies J periods back in a run of t's own XCD (read
+// J * G of its dispatch slots earlier: an L2 hit); the chip streams one front.
+// Blocks past the complete periods map to themselves (remap_tile).
+// a wave-uniform 64-bit value computed on the VALU moved to scalar registers,
+// so it does not hold two VGPRs across the scan
+__device__ __forceinline__ long long uni64(long long v) {
+  const int lo = __builtin_amdgcn_readfirstlane((int)(unsigned)(unsigned long long)v);
+  const int hi = __builtin_amdgcn_readfirstlane((int)(unsigned)((unsigned long long)v >> 32));
+  return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
 struct AheadParams {
@@ -208,15 +204,15 @@ struct AheadParams {
   int k;
   int halo_units;   // ceil(k / F): the stage starts halo_units*F frames before the tile
   int xk_off;       // (-k*C) mod VE
-  int xcd_remap;    // remap mode (remap_tile), or kRemapPeriod (period_tile)
-  unsigned pfull;   // kRemapPeriod: blocks of the complete periods
-  long long pden;   // kRemapPeriod: 8 J T
+  int xcd_remap;    // remap mode (remap_tile): 1, or G (runs of G tiles)
   int ahead;        // D (a multiple of 8): block b publishes the records of block b + D's tile
   int head;         // whole tiles a window can span (k / T): the head duty of remap mode 1
   int spin;         // polls of an untagged granule before recomputing it
   int pre;          // frames in front of `in` that are readable signal (load_elem)
   int eio;          // frame-unit launch on element-aligned pointers (UnitIO::gload)
   unsigned long long* gran;  // [nfull][C][NG] granules, zeroed before the launch
+  unsigned long long* runs;  // RUNS: [runs_done][C][NGA] run totals, zeroed before the launch
+  long long runs_done;       // RUNS: runs [0, runs_done) get a published total
   void* stats;               // MAVG_AHEAD_STATS builds only: {recomputes, polls that waited}
   OutParams o;
 };
@@ -244,6 +240,84 @@ __device__ __forceinline__ void wave_record_lean(const T* __restrict__ in, long 
   for (int c = 0; c < C; ++c) r[c] = readlane(wave_incl_scan(ls[c]), 63);
 }
 
+// A per-tile record (the NW wave shares added in wave order) from the input,
+// one unit in registers at a time: the producer's value, bit for bit.
+template <typename T, typename SA, int C, int F, int U, int WG>
+__device__ __forceinline__ void tile_record_lean(const T* __restrict__ in, long long j, int lane, bool eio,
+                                                 SA (&r)[C]) {
+#pragma unroll 1
+  for (int wv = 0; wv < WG / 64; ++wv) {
+    SA rw[C];
+    wave_record_lean<T, SA, C, F, U, WG>(in, j, wv, lane, eio, rw);
+#pragma unroll
+    for (int c = 0; c < C; ++c) r[c] = wv == 0 ? rw[c] : r[c] + rw[c];
+  }
+}
+
+// RUNS: the total of run rr (tiles [rs, rs + G), G <= 64) in A, by one wave:
+// lane l takes tile rs + l's per-tile record (its granules, polled like the
+// carry's, recomputed from the input when still untagged), then one DPP wave
+// scan.  Producers and the consumers' recompute path both run this: the same
+// bits whoever computes it.
+template <typename T, typename A, int C, int F, int U, int WG>
+__device__ __forceinline__ void run_total(const T* __restrict__ in, const gran_t* gran, long long rs, int G,
+                                          int spin, int lane, bool eio, A (&tot)[C], void* stats = nullptr) {
+  using SA = typename ScanAcc<T, A>::type;
+  constexpr int NG = GranCount<SA>::n;
+  MAVG_DCHECK(G >= 1 && G <= 64, "run length", G, rs);
+  const bool act = lane < G;
+  const long long j = rs + lane;
+  unsigned long long w[C][NG];
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int h = 0; h < NG; ++h) w[c][h] = act ? gran_load(gran + (j * C + c) * NG + h) : 0ull;
+  bool miss = false;
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int h = 0; h < NG; ++h) miss |= act && (w[c][h] >> 32) != 1ull;
+#pragma unroll 1
+  for (int it = 0; __any(miss) && it < spin; ++it) {
+#ifdef MAVG_AHEAD_STATS
+    if (lane == 0 && stats != nullptr) atomicAdd(reinterpret_cast<unsigned int*>(stats) + 2, 1u);
+#endif
+    __builtin_amdgcn_s_sleep(2);
+    if (miss) {
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int h = 0; h < NG; ++h) w[c][h] = gran_load(gran + (j * C + c) * NG + h);
+    }
+    miss = false;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int h = 0; h < NG; ++h) miss |= act && (w[c][h] >> 32) != 1ull;
+  }
+  unsigned long long mask = __ballot(miss);
+#pragma unroll 1
+  while (mask != 0ull) {
+    const int l = __builtin_ctzll(mask);
+    mask &= mask - 1ull;
+    SA r[C];
+    tile_record_lean<T, SA, C, F, U, WG>(in, rs + l, lane, eio, r);
+    if (lane == l)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int h = 0; h < NG; ++h) w[c][h] = kGranTag | gran_word(r[c], h);
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    uint32_t wd[NG];
+#pragma unroll
+    for (int h = 0; h < NG; ++h) wd[h] = (uint32_t)w[c][h];
+    const A v = act ? (A)gran_value<SA>(wd) : (A)0;
+    tot[c] = readlane(wave_incl_scan(v), 63);
+  }
+}
+
 // RC: keep the own tile's registers (U*F*C samples) across the second barrier
 //     and rebuild the in-lane prefix at the output from them and the stage,
 //     instead of keeping U*F*C accumulators (fewer registers for fp32, whose
@@ -258,10 +332,20 @@ __device__ __forceinline__ void wave_record_lean(const T* __restrict__ in, long 
 //     form: the tile is also staged in LDS, lane l holds frames l, l+64, ...
 //     of its 64F-frame wave segment, a 6-step DPP log-step scan per register,
 //     O(n log n) work); the record carry is the same.  RC must be off.
+// RUNS: window-matched runs only (remap mode G, per-tile records): the carry
+//     reads the totals of the whole runs inside the window (~8J of them)
+//     plus the tile records of the partial runs at its two ends (< 2g),
+//     instead of all k/T tile records.  Run rr's total is published by the
+//     block that publishes the record of the last tile of run rr + 8 (the
+//     same XCD's next run, g slots later, when run rr's records are out).
+#ifndef MAVG_AHEAD_RUNS_MINB  // tuning builds: workgroups per CU the RUNS kernel is compiled for
+#define MAVG_AHEAD_RUNS_MINB 1
+#endif
 template <typename T, typename A, int C, int F, int U, int NT, bool RC = false, bool DMA = true, bool WREC = false,
-          int DV = 0, bool HS = false>
-__global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
+          int DV = 0, bool HS = false, bool RUNS = false>
+__global__ __launch_bounds__(kWG, RUNS ? MAVG_AHEAD_RUNS_MINB : 1) void ahead_scan_kernel(AheadParams p) {
   static_assert(!(HS && RC), "the Hillis-Steele flavour keeps its per-element prefixes");
+  static_assert(!(RUNS && WREC), "run totals sum per-tile records");
   constexpr int WG = kWG;
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
@@ -273,6 +357,8 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
   using U_t = Unit<T, VE>;
   using SA = typename ScanAcc<T, A>::type;
   constexpr int NG = GranCount<SA>::n;
+  constexpr int NGA = GranCount<A>::n;                  // granules of a run total
+  constexpr int NGI = RUNS && NGA > NG ? NGA : NG;      // granules of a carry item
   constexpr bool kDma = DMA && IO::kVec && VE * (int)sizeof(T) == 16;
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -297,10 +383,7 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
   const int pre = p.pre;
   const bool eio = F == 1 && p.eio != 0;
 
-  auto map_tile = [&](unsigned b) -> long long {
-    return p.xcd_remap == kRemapPeriod ? period_tile(b, (unsigned long long)p.k, (unsigned long long)p.pden, p.pfull)
-                                       : remap_tile(b, gridDim.x, p.xcd_remap);
-  };
+  auto map_tile = [&](unsigned b) -> long long { return remap_tile(b, gridDim.x, p.xcd_remap); };
   const long long tile = map_tile(blockIdx.x);
   const long long t0 = tile * TF;
   const int Ha = p.halo_units * F;
@@ -312,6 +395,41 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
   constexpr int RPT = WREC ? NW : 1;                            // records per tile
   const long long qlo = jlo * RPT, qhi = tile * RPT;            // records of the whole tiles [jlo, tile)
   const int pcount = a >= 0 ? (int)(jlo * TF - a) : 0;          // window frames before tile jlo (< TF)
+  // the carry's items: [0, n1) records qlo + q, [n1, n1 + nR) run totals
+  // r1 + q - n1 (RUNS), [n1 + nR, nitem) records rs2 + q - n1 - nR
+  long long n1 = qhi - qlo, nR = 0, r1 = 0, rs2 = qhi;
+  if constexpr (RUNS) {  // runs of G tiles: [ra1, rb) lie whole inside the window and have totals
+    const long long G = p.xcd_remap;
+    const long long ra1 = (jlo + G - 1) / G;
+    long long rb = tile / G;
+    rb = rb < p.runs_done ? rb : p.runs_done;
+    if (rb > ra1) {
+      n1 = ra1 * G - jlo;
+      nR = rb - ra1;
+      r1 = ra1;
+      rs2 = rb * G;
+    }
+    n1 = uni64(n1);
+    nR = uni64(nR);
+    r1 = uni64(r1);
+    rs2 = uni64(rs2);
+  }
+  const long long nitem = n1 + nR + (qhi - rs2);
+  auto item_load = [&](long long q, unsigned long long (&v)[C][NGI]) {
+    if (RUNS && q >= n1 && q < n1 + nR) {
+      const long long r = r1 + (q - n1);
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int h = 0; h < NGI; ++h) v[c][h] = gran_load((const gran_t*)p.runs + (r * C + c) * NGA + h);
+    } else {
+      const long long j = q < n1 ? qlo + q : rs2 + (q - n1 - nR);
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int h = 0; h < NGI; ++h) v[c][h] = h < NG ? gran_load(gran + (j * C + c) * NG + h) : kGranTag;
+    }
+  };
 
   // ---- 1. loads: the tile, the shifted tile, phase A's tile (tile t + D:
   //         default policy, it stays in L2), then the first round of records
@@ -404,14 +522,18 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
     wave_record_lean<T, SA, C, F, U, WG>(in, jh, w, lane, eio, r);
     share(2, jh, r);
   }
-  unsigned long long rv[C][NG];
+  unsigned long long rv[C][NGI];
   {
-    const long long q = qlo + tid;
     MAVG_DCHECK(qhi <= p.nfull * RPT, "record read range", qhi, p.nfull);
+    MAVG_DCHECK(!RUNS || (n1 >= 0 && nR >= 0 && rs2 <= qhi && r1 + nR <= p.runs_done), "carry items", n1, nR);
+    if (tid < nitem) {
+      item_load(tid, rv);
+    } else {
 #pragma unroll
-    for (int c = 0; c < C; ++c)
+      for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int h = 0; h < NG; ++h) rv[c][h] = q < qhi ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
+        for (int h = 0; h < NGI; ++h) rv[c][h] = 0ull;
+    }
   }
   if constexpr (HS) {
 #pragma unroll
@@ -431,6 +553,33 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
         for (int i = 1; i < NW; ++i) r[c] += shares[(w * NW + i) * C + c];
       }
       publish_record<SA, C>(gran, j, r, lane);
+    }
+  }
+  if constexpr (RUNS) {
+    // run totals: wave 3 for the record published from phase A, wave 2 for
+    // the block's own; the record's tile is the last of run rr + 8, the same
+    // XCD's next run
+    if (w >= 2) {
+      const long long j = w == 3 ? (produce ? ja : -1) : (own ? tile : -1);
+      const long long G = p.xcd_remap;
+      if (j >= 0 && (j + 1) % G == 0) {
+        const long long rr = (j + 1) / G - 1 - 8;
+        if (rr >= 0 && rr < p.runs_done) {
+          A tot[C];
+          run_total<T, A, C, F, U, WG>(in, gran, rr * G, (int)G, p.spin, lane, eio, tot, p.stats);
+#ifdef MAVG_AHEAD_STATS
+          if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats) + 3, 1u);
+#endif
+          if (lane < C * NGA) {
+            const int c = lane / NGA, h = lane - c * NGA;
+            A v = tot[0];
+#pragma unroll
+            for (int i = 1; i < C; ++i)
+              if (c == i) v = tot[i];
+            gran_store((gran_t*)p.runs + (rr * C + c) * NGA + h, gran_word(v, h));
+          }
+        }
+      }
     }
   }
 
@@ -545,37 +694,36 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
 #pragma unroll
   for (int c = 0; c < C; ++c) hq[c] = (A)0;
 #pragma unroll 1
-  for (long long qb = qlo; qb < qhi; qb += WG) {
+  for (long long qb = 0; qb < nitem; qb += WG) {
     const long long q = qb + tid;
-    const bool act = q < qhi;
-    if (qb != qlo) {
+    const bool act = q < nitem;
+    if (qb != 0) {
+      if (act) {
+        item_load(q, rv);
+      } else {
 #pragma unroll
-      for (int c = 0; c < C; ++c)
+        for (int c = 0; c < C; ++c)
 #pragma unroll
-        for (int h = 0; h < NG; ++h) rv[c][h] = act ? gran_load(gran + (q * C + c) * NG + h) : 0ull;
+          for (int h = 0; h < NGI; ++h) rv[c][h] = 0ull;
+      }
     }
     bool miss = false;
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int h = 0; h < NG; ++h) miss |= act && (rv[c][h] >> 32) != 1ull;
+      for (int h = 0; h < NGI; ++h) miss |= act && (rv[c][h] >> 32) != 1ull;
 #pragma unroll 1
     for (int it = 0; __any(miss) && it < p.spin; ++it) {
 #ifdef MAVG_AHEAD_STATS
       if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats) + 1, 1u);
 #endif
       __builtin_amdgcn_s_sleep(2);
-      if (miss) {
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-#pragma unroll
-          for (int h = 0; h < NG; ++h) rv[c][h] = gran_load(gran + (q * C + c) * NG + h);
-      }
+      if (miss) item_load(q, rv);
       miss = false;
 #pragma unroll
       for (int c = 0; c < C; ++c)
 #pragma unroll
-        for (int h = 0; h < NG; ++h) miss |= act && (rv[c][h] >> 32) != 1ull;
+        for (int h = 0; h < NGI; ++h) miss |= act && (rv[c][h] >> 32) != 1ull;
     }
     // still untagged: the wave recomputes each such record from the input,
     // with the producer's lane mapping and order of operations
@@ -584,36 +732,58 @@ __global__ __launch_bounds__(kWG) void ahead_scan_kernel(AheadParams p) {
     while (mask != 0ull) {
       const int l = __builtin_ctzll(mask);
       mask &= mask - 1ull;
-      const long long jj = __shfl(q, l, 64);
-      SA r[C];
-      if constexpr (WREC) {  // record jj = (tile, wave)
-        wave_record_lean<T, SA, C, F, U, WG>(in, jj / NW, (int)(jj % NW), lane, eio, r);
+      const long long qq = __shfl(q, l, 64);
+      if (RUNS && qq >= n1 && qq < n1 + nR) {  // a run total: the producer's sequence
+        const long long G = p.xcd_remap;
+        A tot[C];
+        run_total<T, A, C, F, U, WG>(in, gran, (r1 + (qq - n1)) * G, (int)G, p.spin, lane, eio, tot);
+        if (lane == l)
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int h = 0; h < NGI; ++h) rv[c][h] = kGranTag | gran_word(tot[c], h);
       } else {
-#pragma unroll 1
-        for (int wv = 0; wv < NW; ++wv) {
-          SA rw[C];
-          wave_record_lean<T, SA, C, F, U, WG>(in, jj, wv, lane, eio, rw);
-#pragma unroll
-          for (int c = 0; c < C; ++c) r[c] = wv == 0 ? rw[c] : r[c] + rw[c];
+        const long long jj = RUNS ? (qq < n1 ? qlo + qq : rs2 + (qq - n1 - nR)) : qlo + qq;
+        SA r[C];
+        if constexpr (WREC) {  // record jj = (tile, wave)
+          wave_record_lean<T, SA, C, F, U, WG>(in, jj / NW, (int)(jj % NW), lane, eio, r);
+        } else {
+          tile_record_lean<T, SA, C, F, U, WG>(in, jj, lane, eio, r);
         }
+        if (lane == l)
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int h = 0; h < NGI; ++h) rv[c][h] = kGranTag | (h < NG ? gran_word(r[c], h) : 0u);
       }
-      if (lane == l)
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-#pragma unroll
-          for (int h = 0; h < NG; ++h) rv[c][h] = kGranTag | gran_word(r[c], h);
 #ifdef MAVG_AHEAD_STATS
       if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats), 1u);
 #endif
     }
-    if (act)
+    if (act) {
+      const bool run_item = RUNS && q >= n1 && q < n1 + nR;
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        uint32_t wd[NG];
+        if constexpr (RUNS && NGA > NG) {
+          uint32_t wa[NGA], ws[NG];
 #pragma unroll
-        for (int h = 0; h < NG; ++h) wd[h] = (uint32_t)rv[c][h];
-        hq[c] += (A)gran_value<SA>(wd);
+          for (int h = 0; h < NGA; ++h) wa[h] = (uint32_t)rv[c][h];
+#pragma unroll
+          for (int h = 0; h < NG; ++h) ws[h] = (uint32_t)rv[c][h];
+          hq[c] += run_item ? gran_value<A>(wa) : (A)gran_value<SA>(ws);
+        } else if constexpr (RUNS) {  // NGA == NG
+          uint32_t wd[NGI];
+#pragma unroll
+          for (int h = 0; h < NGI; ++h) wd[h] = (uint32_t)rv[c][h];
+          hq[c] += run_item ? gran_value<A>(wd) : (A)gran_value<SA>(wd);
+        } else {
+          uint32_t wd[NG];
+#pragma unroll
+          for (int h = 0; h < NG; ++h) wd[h] = (uint32_t)rv[c][h];
+          hq[c] += (A)gran_value<SA>(wd);
+        }
       }
+    }
   }
 #pragma unroll
   for (int c = 0; c < C; ++c) {

@@ -269,28 +269,39 @@ def test_grouped_xcd_remap_with_tail(oracle_mod, gpu, dtype, C, k):
         assert np.array_equal(_run(x, k, C, "auto", gpu), oracle_mod.mavg_i16(x, k, C)), plan
 
 
-@pytest.mark.parametrize("dtype,C,k", [("f32", 1, 600_000), ("i16", 2, 1_000_000), ("f32", 1, 4_000_000)])
-def test_period_remap_very_long_windows_with_tail(oracle_mod, gpu, dtype, C, k):
+@pytest.mark.parametrize("dtype,C,k,algo", [("f32", 1, 600_000, "auto"), ("i16", 2, 1_000_000, "auto"),
+                                            ("f32", 1, 4_000_000, "auto"), ("f32", 4, 300_000, "auto"),
+                                            ("f32", 1, 700_000, "hillis"), ("f32", 1, 2_000_000, "auto"),
+                                            ("i16", 2, 1_700_000, "auto"), ("i16", 1, 1_500_000, "auto")])
+def test_period_remap_very_long_windows_with_tail(oracle_mod, gpu, dtype, C, k, algo):
     """Windows past the L2 reach: the look-ahead scan runs in window-matched
-    runs (period_tile: J periods of 8 runs per window, run lengths floor/ceil
-    of k/(8JT)); two periods and a ragged tail past them (blocks mapped to
-    themselves), every output against the oracle."""
+    runs of G tiles per XCD (remap mode G, 8JG ~ k/T, G not a power of two:
+    remap_tile's divide path) and its carry reads run totals for the whole
+    runs inside the window (runs=1); more than a window and three periods,
+    and a ragged tail past them (blocks mapped to themselves), every output
+    against the oracle, and bitwise the same output when every record and run
+    total is recomputed by its consumer or the look-ahead is cut to 0 / 8."""
     import digital_signal_processsing_amd as dsp
     code = dsp.F32 if dtype == "f32" else dsp.I16
-    plan = dsp.plan(1 << 30, k, C, code)
-    remap = plan.split("remap=")[1].split()[0]
+    plan = dsp.plan(1 << 30, k, C, code, algo)
+    G = int(plan.split("remap=")[1].split()[0])
     tile = int(plan.split("tile_frames=")[1].split()[0])
-    assert plan.startswith("ahead_scan<") and remap.startswith("period"), plan
-    J = int(remap[len("period"):])
-    frames = int(tile * (2 * k / (tile * J) + 37)) + 5  # two periods of k/J frames and a ragged tail
-    assert dsp.plan(frames * C, k, C, code).split("remap=")[1].split()[0] == remap
+    assert plan.startswith("ahead_scan<") and G > 1, plan
+    assert ("runs=1" in plan) == (C <= 2 and algo == "auto" and k > 384 * tile), plan
+    frames = tile * max(3 * 8 * G + 37, k // tile + 8 * G + 37) + 5  # past one window, 3 periods, a ragged tail
+    assert int(dsp.plan(frames * C, k, C, code, algo).split("remap=")[1].split()[0]) == G
     if dtype == "f32":
         x = oracle_mod.synth_f32(frames * C, dist=2)  # offset 0: the checker's stream starts at the signal's start
-        r = oracle_mod.check_synth_exact(_run(x, k, C, "auto", gpu), k, C, dist=2)
-        assert r["mismatches"] == 0, (plan, r)
+        base = _run(x, k, C, algo, gpu)
+        r = oracle_mod.check_synth_exact(base, k, C, dist=2)
+        assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, (plan, r)
     else:
         x = oracle_mod.synth_i16(frames * C, offset=77)
-        assert np.array_equal(_run(x, k, C, "auto", gpu), oracle_mod.mavg_i16(x, k, C)), plan
+        base = _run(x, k, C, algo, gpu)
+        assert np.array_equal(base, oracle_mod.mavg_i16(x, k, C)), plan
+    for sched in ({"spin": 0}, {"slots": 0}, {"slots": 8, "spin": 0}):
+        y = _with_schedule(sched, lambda: _run(x, k, C, algo, gpu))
+        assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), sched
 
 
 def test_many_channels_auto(oracle_mod, gpu):

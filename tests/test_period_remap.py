@@ -1,29 +1,15 @@
-"""The tile -> workgroup mappings of the look-ahead scan, restated on the host
-(specification tests; the device code is digital_signal_processsing_amd/csrc/
-mavg_lookback.hpp period_tile and mavg_device.hpp remap_tile, exercised on the
-GPU by test_gpu_parity.py::test_period_remap_very_long_windows_with_tail and
-test_grouped_xcd_remap_with_tail): bijective over every grid, and for
-window-matched runs x[n-k]'s tile runs on the tile's own XCD."""
+"""The tile -> workgroup mapping of the look-ahead scan for windows past an
+XCD's L2 reach, restated on the host (specification tests; the device code is
+digital_signal_processsing_amd/csrc/mavg_device.hpp remap_tile, exercised on
+the GPU by test_gpu_parity.py::test_period_remap_very_long_windows_with_tail
+and test_grouped_xcd_remap_with_tail): runs of G tiles per XCD, bijective over
+every grid, and G matched to the window so that x[n-k]'s tile runs on the
+tile's own XCD; the launcher's choice of G (ahead_run_length, mavg_launch.hpp)."""
 import re
 
 import pytest
 
 TF = 4096
-
-
-def period_tile(b, k, pden, pfull):
-    if b >= pfull:
-        return b
-    i, x = b >> 3, b & 7
-    per = ((i + 1) * pden - 1) // k
-    s0, s1 = per * k // pden, (per + 1) * k // pden
-    return 8 * s0 + x * (s1 - s0) + (i - s0)
-
-
-def period_params(k, J, nb):
-    pden = 8 * J * TF
-    P = ((nb // 8 + 1) * pden - 1) // k
-    return pden, 8 * (P * k // pden)
 
 
 def remap_group(b, nb, G):
@@ -35,36 +21,52 @@ def remap_group(b, nb, G):
     return per * 8 * G + x * G + (i - per * G)
 
 
-@pytest.mark.parametrize("k", [524_289, 600_000, 1_000_000, 2_222_222, 4_000_000])
-@pytest.mark.parametrize("J", [1, 2, 3])
-@pytest.mark.parametrize("nb", [8 * 1000 + 5, 262_144, 262_181])
-def test_period_tile_is_a_bijection_with_same_xcd_shift(k, J, nb):
-    pden, pfull = period_params(k, J, nb)
-    tiles = [period_tile(b, k, pden, pfull) for b in range(nb)]
-    assert sorted(tiles) == list(range(nb))
-    assert pfull % 8 == 0 and pfull <= nb
-    blk = {t: b for b, t in enumerate(tiles)}
-    inside = [t for t in range(nb) if blk[t] < pfull and t * TF >= k and blk[(t * TF - k) // TF] < pfull]
-    same = sum(blk[t] % 8 == blk[(t * TF - k) // TF] % 8 for t in inside)
-    # a run of ~g = k/(8 J T) tiles holds the shifted tile except near a run
-    # boundary: run x of a period starts x * (G_p - G_{p-J}) tiles (at most
-    # x <= 7, the floor/ceil run lengths) off its place J periods back, so the
-    # misses grow with J and shrink with g (J = 1, k = 10^6: 7 %)
-    g = k / (8 * J * TF)
-    assert same / len(inside) >= 1 - (J + 2.5) / g, (same / len(inside), g)
+def run_length(k, tf, ahead):
+    """ahead_run_length (mavg_launch.hpp)."""
+    gmax = max(2, min(48, ahead // 20))
+    m = k / tf
+    J = 1
+    while m / (8.0 * J) > gmax + 0.5:
+        J += 1
+    best, best_miss = 0, 2.0
+    for j in range(J, J + 8):
+        G = max(2, int(m / (8.0 * j) + 0.5))
+        miss = abs(m - 8.0 * j * G) / G
+        if G <= gmax and miss < best_miss - 1e-9:
+            best_miss, best = miss, G
+    return best or gmax
 
 
-@pytest.mark.parametrize("G", [2, 3, 18, 31, 61, 64])
+@pytest.mark.parametrize("G", [2, 3, 18, 23, 31, 41, 64])
 @pytest.mark.parametrize("nb", [7, 8 * 61 + 3, 262_144, 262_181])
-def test_grouped_runs_are_a_bijection(G, nb):
+def test_runs_are_a_bijection(G, nb):
     assert sorted(remap_group(b, nb, G) for b in range(nb)) == list(range(nb))
+
+
+@pytest.mark.parametrize("k,ahead", [(524_289, 1024), (600_000, 1024), (1_000_000, 1024), (2_222_222, 1024),
+                                     (4_000_000, 1024), (1_000_000, 768), (10_000_000, 1024)])
+def test_matched_runs_put_the_shifted_tile_on_the_same_xcd(k, ahead):
+    nb = 262_144
+    G = run_length(k, TF, ahead)
+    assert 2 <= G <= min(48, ahead // 20)
+    blk = {remap_group(b, nb, G): b for b in range(nb)}
+    full = nb - nb % (8 * G)
+    inside = [t for t in range(nb) if t * TF >= k and blk[t] < full and blk[(t * TF - k) // TF] < full]
+    same = sum(blk[t] % 8 == blk[(t * TF - k) // TF] % 8 for t in inside) / len(inside)
+    m = k / TF
+    J = max(1, round(m / (8 * G)))
+    miss = abs(m - 8 * J * G) / G
+    assert same >= 1 - miss - 1.5 / G, (G, J, same, miss)
 
 
 def test_plans_pick_window_matched_runs_past_the_l2_reach():
     import digital_signal_processsing_amd as dsp
-    remap = lambda k, C, dt: re.search(r"remap=(\S+)", dsp.plan(1 << 30, k, C, dt)).group(1)
-    assert remap(44_100, 1, dsp.F32) == "1" and remap(300_000, 1, dsp.F32) == "1"
-    assert remap(1_000_000, 1, dsp.F32) == "period1"
-    assert remap(4_000_000, 1, dsp.F32) == "period4"
-    assert remap(1_000_000, 2, dsp.I16) == "period1"
-    assert remap(1024, 1, dsp.F32) == "64"  # the tile kernel's grouped runs
+    plan = lambda k, C, dt: dsp.plan(1 << 30, k, C, dt)
+    remap = lambda k, C, dt: int(re.search(r"remap=(\d+)", plan(k, C, dt)).group(1))
+    assert remap(44_100, 1, dsp.F32) == 1 and remap(300_000, 1, dsp.F32) == 1
+    for k, C, dt, tf, ahead in ((600_000, 1, dsp.F32, 4096, 1024), (1_000_000, 1, dsp.F32, 4096, 1024),
+                                (4_000_000, 1, dsp.F32, 4096, 1024), (1_000_000, 2, dsp.I16, 4096, 768),
+                                (1_500_000, 1, dsp.I16, 8192, 1024)):
+        assert remap(k, C, dt) == run_length(k, tf, ahead), (k, C)
+        assert ("runs=1" in plan(k, C, dt)) == (k > 384 * tf), (k, C)
+    assert remap(1024, 1, dsp.F32) == 64  # the tile kernel's grouped runs
