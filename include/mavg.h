@@ -88,7 +88,8 @@ typedef enum {
  * per-wave records, padded to 16, + 16, sized for the smaller tiles of the
  * frame-unit form a misaligned view may run (2^30 fp32 mono samples: 64 MiB
  * at k=8192..44100 with per-wave records, 16 MiB at k=10^6 with per-tile
- * records; int16 stereo k=44100: 8 MiB).
+ * records; int16 stereo k=44100: 8 MiB), + the run totals of windows past
+ * 384 tiles (8 B per run of G tiles per channel word: < 1 % more).
  * 16-B alignment; contents need no initialisation (mavg_run zeroes them on
  * the stream); one workspace must not serve two launches that may run
  * concurrently. */
@@ -109,7 +110,7 @@ int mavg_workspace_bytes(size_t n_samples, int channels, int grade, int dtype,
  *              scans and the direct kernel run the next power of two of at
  *              least one wave64 (64, 128, 256, 512, 1024), while the window's
  *              halo fits that workgroup's LDS (longer windows keep the tuned
- *              look-ahead / segment scan).  mavg_plan() shows the result.
+ *              look-ahead scan).  mavg_plan() shows the result.
  *   stream     hipStream_t or NULL.
  * Returns a mavg_status.  Nothing is enqueued unless MAVG_OK is returned
  * (MAVG_ERR_HIP excepted, when the launch itself failed).

@@ -41,6 +41,9 @@ for step in "$@"; do
             --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --check &&
           run dist4 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
             --master-port 29512 bench.py --gpus 4 --steps 3 --warmup 1 --dist-backend gloo --check ;;
+    dist2) run pytest_dist2 600 python -u -m pytest tests/test_gpu_fullsize.py -m gpu -k rounding -s -q \
+            --timeout 170 --timeout-method thread -p no:cacheprovider ;;
+    dab) run direct_ab 200 bash tools/gpu/r03_direct_ab.sh "$TAG" ;;
     full) run pytest_full 900 python -u -m pytest tests/test_gpu_fullsize.py tests/test_bench_launch.py -m gpu -x -v \
             --timeout 170 --timeout-method thread -p no:cacheprovider ;;
     # the driver's exact bench command, then the same command under the kernel tracer
