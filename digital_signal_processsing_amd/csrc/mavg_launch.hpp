@@ -198,8 +198,9 @@ inline bool ahead_past_l2(long long k, int C, int elem, int TF) {
   return k * C * elem > (1LL << 21) && k >= 8LL * TF;
 }
 template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0, bool HS = false,
-          bool RUNS = false>
+          bool RUNS = false, int WG = kWG>
 int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
+  constexpr int NW = WG / 64;
   const long long nframes = sg.nframes;
   {
     const int t = g_test_ahead_slots.load(std::memory_order_relaxed);
@@ -218,7 +219,7 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   // Measured, 2^30 fp32 (profiles/r03_tuning/remap/, period/): one run per
   // XCD -> runs of 64 tiles -> window-matched runs: k=4e6 0.185 -> 0.526;
   // k=1e6 0.524 -> 0.588 -> 0.668; k=6e5 0.594 -> 0.599 -> 0.681
-  constexpr int TF = kWG * F * U;
+  constexpr int TF = WG * F * U;
 #ifdef MAVG_AHEAD_FIXED_RUN
   const int xcd_remap = ahead_past_l2(k, C, sizeof(T), TF) ? MAVG_AHEAD_FIXED_RUN : 1;
   static_assert(!RUNS, "run totals need window-matched runs");
@@ -227,9 +228,9 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   if (RUNS && xcd_remap == 1) return MAVG_ERR_UNSUPPORTED;
 #endif
   constexpr int VE = F * C;
-  constexpr int NSEG = U * kNW;
+  constexpr int NSEG = U * NW;
   using SA = typename ScanAcc<T, A>::type;
-  constexpr size_t kStageBytes = (((size_t)(U * kWG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15;
+  constexpr size_t kStageBytes = (((size_t)(U * WG + 1) * VE * sizeof(T)) + 15) & ~(size_t)15;
   const long long ntiles = (nframes + TF - 1) / TF;
   const long long nfull = nframes / TF;
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
@@ -239,18 +240,18 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   const long long P = xcd_remap > 1 ? ntiles / (8LL * xcd_remap) : 0;
   const long long pub_periods = P - 1 - (8LL * xcd_remap * P > nfull ? 1 : 0);
   const long long runs_done = RUNS && pub_periods > 0 ? 8 * pub_periods : 0;
-  const size_t rec_bytes = ahead_granule_bytes<T, A, C, F, U>(nfull * (WREC ? kNW : 1)) - 16;
+  const size_t rec_bytes = ahead_granule_bytes<T, A, C, F, U>(nfull * (WREC ? NW : 1)) - 16;
   const size_t run_bytes = ((size_t)runs_done * C * GranCount<A>::n * 8 + 15) / 16 * 16;
   const size_t need = rec_bytes + run_bytes + 16;
-  size_t lds = kStageBytes + (size_t)kNW * C * sizeof(A) + (size_t)(NSEG + 3 * kNW) * C * sizeof(SA);
-  if (HS) lds = (lds + 15) / 16 * 16 + (size_t)U * kWG * VE * sizeof(T);  // + the tile itself (HS)
+  size_t lds = kStageBytes + (size_t)NW * C * sizeof(A) + (size_t)(NSEG + 3 * NW) * C * sizeof(SA);
+  if (HS) lds = (lds + 15) / 16 * 16 + (size_t)U * WG * VE * sizeof(T);  // + the tile itself (HS)
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
              "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dma=%d,wrec=%d,dv=%d> grid=%lld block=%d lds=%zu "
              "tile_frames=%d ahead=%d remap=%d%s ws=%zu",
              type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC, (int)DMA, (int)WREC, DV,
-             ntiles, kWG, lds, TF, ahead, xcd_remap, RUNS ? " runs=1" : "", need);
+             ntiles, WG, lds, TF, ahead, xcd_remap, RUNS ? " runs=1" : "", need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -277,8 +278,8 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.gran = static_cast<unsigned long long*>(ws.ptr);
   p.runs = reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(ws.ptr) + rec_bytes);
   p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
-  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV, HS, RUNS>), dim3((unsigned)ntiles),
-                     dim3(kWG), lds, st, p);
+  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV, HS, RUNS, WG>), dim3((unsigned)ntiles),
+                     dim3(WG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
@@ -291,29 +292,35 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
 //     fp32 keeps the tile in registers across the second barrier (RC, fewer
 //     live fp64 accumulators)
 //   otherwise: per-tile records, D = 768 (stereo int16) / 1024
-template <typename T, typename A, int C, int F, bool HS = false, int U = 4>
+#ifndef MAVG_AHEAD_WG  // tuning builds: workgroup size of the look-ahead scan (the tile stays U*256 units)
+#define MAVG_AHEAD_WG kWG
+#endif
+template <typename T, typename A, int C, int F, bool HS = false, int U0 = 4>
 int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
-  constexpr int TF = kWG * F * U;
+  constexpr int WG = MAVG_AHEAD_WG;
+  constexpr int U = U0 * kWG / WG;
+  static_assert(U >= 1 && U * WG == U0 * kWG, "look-ahead tile of U0 x 256 units");
+  constexpr int TF = WG * F * U;
   constexpr int kNtA = kNtStore | kNtHalo;
   constexpr bool kRC = sizeof(T) == 4 && C == 1 && !HS;
   constexpr int D = C == 2 ? 768 : 1024;
   int s;
-  if (C == 1 && (long long)k / TF + 1 <= kWG / kNW)
-    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true, 0, HS>(sg, k, st, ws, 512);
+  if (C == 1 && (long long)k / TF + 1 <= 64)
+    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true, 0, HS, false, WG>(sg, k, st, ws, 512);
 #if !defined(MAVG_AHEAD_FIXED_RUN) && !defined(MAVG_AHEAD_NO_RUNS)
   // run totals (O(J + G) carry items instead of k/T) where the windows are
   // long enough to pay for the kernel's extra registers (4 waves per SIMD
   // instead of 5): > 384 tiles (A/B, profiles/r03_tuning/runs/: fp32
   // k=4e6 0.543 -> 0.596, k=2e6 0.623 -> 0.641; k=1e6 0.670 -> 0.642)
-  else if (C <= 2 && U == 4 && !HS && ahead_past_l2(k, C, sizeof(T), TF) && (long long)k > 384LL * TF)
-    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS, C <= 2 && U == 4 && !HS>(sg, k, st, ws, D);
+  else if (C <= 2 && U0 == 4 && !HS && ahead_past_l2(k, C, sizeof(T), TF) && (long long)k > 384LL * TF)
+    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS, C <= 2 && U0 == 4 && !HS, WG>(sg, k, st, ws, D);
 #endif
   else
-    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS>(sg, k, st, ws, D);
+    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS, false, WG>(sg, k, st, ws, D);
   // the Hillis-Steele form also stages the tile: wide frames (e.g. 8 fp32
   // channels, 32 B) take half tiles to stay inside the LDS budget
-  if constexpr (HS && U > 2) {
-    if (s == MAVG_ERR_UNSUPPORTED) return dispatch_ahead<T, A, C, F, HS, 2>(sg, k, st, ws);
+  if constexpr (HS && U0 > 2) {
+    if (s == MAVG_ERR_UNSUPPORTED) return dispatch_ahead<T, A, C, F, HS, U0 / 2>(sg, k, st, ws);
   }
   return s;
 }

@@ -342,11 +342,11 @@ __device__ __forceinline__ void run_total(const T* __restrict__ in, const gran_t
 #define MAVG_AHEAD_RUNS_MINB 1
 #endif
 template <typename T, typename A, int C, int F, int U, int NT, bool RC = false, bool DMA = true, bool WREC = false,
-          int DV = 0, bool HS = false, bool RUNS = false>
-__global__ __launch_bounds__(kWG, RUNS ? MAVG_AHEAD_RUNS_MINB : 1) void ahead_scan_kernel(AheadParams p) {
+          int DV = 0, bool HS = false, bool RUNS = false, int WG_ = kWG>
+__global__ __launch_bounds__(WG_, RUNS ? MAVG_AHEAD_RUNS_MINB : 1) void ahead_scan_kernel(AheadParams p) {
   static_assert(!(HS && RC), "the Hillis-Steele flavour keeps its per-element prefixes");
   static_assert(!(RUNS && WREC), "run totals sum per-tile records");
-  constexpr int WG = kWG;
+  constexpr int WG = WG_;
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
   constexpr int TF = WG * F * U;
