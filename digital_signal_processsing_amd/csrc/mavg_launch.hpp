@@ -246,6 +246,9 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   size_t lds = kStageBytes + (size_t)NW * C * sizeof(A) + (size_t)(NSEG + 3 * NW) * C * sizeof(SA);
   if (HS) lds = (lds + 15) / 16 * 16 + (size_t)U * WG * VE * sizeof(T);  // + the tile itself (HS)
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
+#ifdef MAVG_AHEAD_LDS_MIN  // tuning builds: fewer workgroups per CU through a bigger LDS allocation
+  lds = std::max<size_t>(lds, MAVG_AHEAD_LDS_MIN);
+#endif
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
              "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dma=%d,wrec=%d,dv=%d> grid=%lld block=%d lds=%zu "

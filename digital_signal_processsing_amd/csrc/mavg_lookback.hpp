@@ -341,9 +341,16 @@ __device__ __forceinline__ void run_total(const T* __restrict__ in, const gran_t
 #ifndef MAVG_AHEAD_RUNS_MINB  // tuning builds: workgroups per CU the RUNS kernel is compiled for
 #define MAVG_AHEAD_RUNS_MINB 1
 #endif
+#ifndef MAVG_AHEAD_MINB_F32  // tuning builds: the same for the other look-ahead kernels, per dtype
+#define MAVG_AHEAD_MINB_F32 1
+#endif
+#ifndef MAVG_AHEAD_MINB_I16
+#define MAVG_AHEAD_MINB_I16 1
+#endif
 template <typename T, typename A, int C, int F, int U, int NT, bool RC = false, bool DMA = true, bool WREC = false,
           int DV = 0, bool HS = false, bool RUNS = false, int WG_ = kWG>
-__global__ __launch_bounds__(WG_, RUNS ? MAVG_AHEAD_RUNS_MINB : 1) void ahead_scan_kernel(AheadParams p) {
+__global__ __launch_bounds__(WG_, RUNS ? MAVG_AHEAD_RUNS_MINB : (sizeof(T) == 4 ? MAVG_AHEAD_MINB_F32 : MAVG_AHEAD_MINB_I16))
+void ahead_scan_kernel(AheadParams p) {
   static_assert(!(HS && RC), "the Hillis-Steele flavour keeps its per-element prefixes");
   static_assert(!(RUNS && WREC), "run totals sum per-tile records");
   constexpr int WG = WG_;
