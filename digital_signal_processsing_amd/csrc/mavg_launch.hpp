@@ -242,7 +242,12 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   const long long runs_done = RUNS && pub_periods > 0 ? 8 * pub_periods : 0;
   const size_t rec_bytes = ahead_granule_bytes<T, A, C, F, U>(nfull * (WREC ? NW : 1)) - 16;
   const size_t run_bytes = ((size_t)runs_done * C * GranCount<A>::n * 8 + 15) / 16 * 16;
-  const size_t need = rec_bytes + run_bytes + 16;
+#ifdef MAVG_AHEAD_TRACE
+  const size_t trace_bytes = (size_t)ntiles * 64;  // tuning builds: 8 stamps per tile, after the stats
+#else
+  const size_t trace_bytes = 0;
+#endif
+  const size_t need = rec_bytes + run_bytes + 16 + trace_bytes;
   size_t lds = kStageBytes + (size_t)NW * C * sizeof(A) + (size_t)(NSEG + 3 * NW) * C * sizeof(SA);
   if (HS) lds = (lds + 15) / 16 * 16 + (size_t)U * WG * VE * sizeof(T);  // + the tile itself (HS)
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
@@ -280,7 +285,10 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.spin = spin;
   p.gran = static_cast<unsigned long long*>(ws.ptr);
   p.runs = reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(ws.ptr) + rec_bytes);
-  p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
+  p.stats = static_cast<unsigned char*>(ws.ptr) + need - trace_bytes - 16;
+#ifdef MAVG_AHEAD_TRACE
+  p.trace = reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(ws.ptr) + need - trace_bytes);
+#endif
   hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV, HS, RUNS, WG>), dim3((unsigned)ntiles),
                      dim3(WG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;

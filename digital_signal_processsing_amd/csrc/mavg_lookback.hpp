@@ -214,6 +214,9 @@ struct AheadParams {
   unsigned long long* runs;  // RUNS: [runs_done][C][NGA] run totals, zeroed before the launch
   long long runs_done;       // RUNS: runs [0, runs_done) get a published total
   void* stats;               // MAVG_AHEAD_STATS builds only: {recomputes, polls that waited}
+#ifdef MAVG_AHEAD_TRACE
+  unsigned long long* trace;  // tuning builds only: [ntiles][8] phase stamps (tools/tune/ahead_trace.py)
+#endif
   OutParams o;
 };
 
@@ -338,6 +341,17 @@ __device__ __forceinline__ void run_total(const T* __restrict__ in, const gran_t
 //     instead of all k/T tile records.  Run rr's total is published by the
 //     block that publishes the record of the last tile of run rr + 8 (the
 //     same XCD's next run, g slots later, when run rr's records are out).
+// MAVG_AHEAD_TRACE (tuning builds only, tools/tune/ahead_trace.py): per tile,
+// 100-MHz wall-clock stamps of the phases, taken by thread 0
+#ifdef MAVG_AHEAD_TRACE
+#define MAVG_ATRACE(slot, v) \
+  (p.trace[(unsigned long long)tile * 8 + (slot)] = (unsigned long long)(v))
+#define MAVG_ANOW() __builtin_amdgcn_s_memrealtime()
+#else
+#define MAVG_ATRACE(slot, v) ((void)0)
+#define MAVG_ANOW() 0ull
+#endif
+
 #ifndef MAVG_AHEAD_RUNS_MINB  // tuning builds: workgroups per CU the RUNS kernel is compiled for
 #define MAVG_AHEAD_RUNS_MINB 1
 #endif
@@ -397,6 +411,7 @@ void ahead_scan_kernel(AheadParams p) {
   const long long h0 = t0 - Ha;
   MAVG_DCHECK(tile >= 0 && tile < (long long)gridDim.x && t0 < nframes, "ahead tile index", tile, gridDim.x);
   const bool tile_full = (t0 + TF <= nframes);
+  if (tid == 0) MAVG_ATRACE(0, MAVG_ANOW());
   const long long a = t0 - k;                                   // first frame of the window before t0
   const long long jlo = a >= 0 ? (a + TF - 1) / TF : 0;         // first whole tile inside it
   constexpr int RPT = WREC ? NW : 1;                            // records per tile
@@ -507,6 +522,7 @@ void ahead_scan_kernel(AheadParams p) {
     wave_record<T, SA, C, F, U>(xa, r);
     share(0, ja, r);
   }
+  if (tid == 0) MAVG_ATRACE(1, MAVG_ANOW());  // phase A summed (and, WREC, published)
   const bool own = blockIdx.x < (unsigned)p.ahead && tile < p.nfull;  // no block D slots earlier
   if (own) {
     SA r[C];
@@ -547,6 +563,7 @@ void ahead_scan_kernel(AheadParams p) {
     for (int u = 0; u < U; ++u) IO::store(tstage + (u * WG + tid) * VE, x[u]);
   }
   __syncthreads();
+  if (tid == 0) MAVG_ATRACE(2, MAVG_ANOW());  // first barrier
   // publish the records whose wave shares this block holds: wave src adds
   // source src's NW shares in wave order
   if (!WREC && w < 3) {
@@ -697,9 +714,13 @@ void ahead_scan_kernel(AheadParams p) {
   }
 
   // ---- 4. whole-tile carry from the records, WG per round ----
+  if (tid == 0) MAVG_ATRACE(3, MAVG_ANOW());  // in-tile scan done
   A hq[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) hq[c] = (A)0;
+#ifdef MAVG_AHEAD_TRACE
+  unsigned npoll = 0;  // wave 0's polls of untagged carry items
+#endif
 #pragma unroll 1
   for (long long qb = 0; qb < nitem; qb += WG) {
     const long long q = qb + tid;
@@ -723,6 +744,9 @@ void ahead_scan_kernel(AheadParams p) {
     for (int it = 0; __any(miss) && it < p.spin; ++it) {
 #ifdef MAVG_AHEAD_STATS
       if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats) + 1, 1u);
+#endif
+#ifdef MAVG_AHEAD_TRACE
+      ++npoll;
 #endif
       __builtin_amdgcn_s_sleep(2);
       if (miss) item_load(q, rv);
@@ -797,7 +821,9 @@ void ahead_scan_kernel(AheadParams p) {
     const A r = readlane(wave_incl_scan(hp[c] + hq[c]), 63);
     if (lane == 0) hsum[w * C + c] = r;
   }
+  if (tid == 0) MAVG_ATRACE(4, MAVG_ANOW());  // wave 0's carry items read
   __syncthreads();
+  if (tid == 0) MAVG_ATRACE(5, MAVG_ANOW());  // second barrier
 
   // ---- 5. carry + earlier segments; outputs ----
   static_assert(NSEG <= 64, "segment totals are scanned across one wave");
@@ -864,6 +890,12 @@ void ahead_scan_kernel(AheadParams p) {
           for (int c = 0; c < C; ++c) out[(f + fr) * C + c] = y.e[fr * C + c];
     }
   }
+#ifdef MAVG_AHEAD_TRACE
+  if (tid == 0) {
+    MAVG_ATRACE(6, MAVG_ANOW());  // outputs issued
+    MAVG_ATRACE(7, (unsigned long long)npoll);
+  }
+#endif
 }
 
 }  // namespace mavg
