@@ -199,7 +199,7 @@ inline bool ahead_past_l2(long long k, int C, int elem, int TF) {
 }
 template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0, bool HS = false,
           bool RUNS = false, int WG = kWG>
-int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
+int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead, bool self = false) {
   constexpr int NW = WG / 64;
   const long long nframes = sg.nframes;
   {
@@ -257,9 +257,9 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
              "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dma=%d,wrec=%d,dv=%d> grid=%lld block=%d lds=%zu "
-             "tile_frames=%d ahead=%d remap=%d%s ws=%zu",
+             "tile_frames=%d ahead=%d remap=%d%s%s ws=%zu",
              type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC, (int)DMA, (int)WREC, DV,
-             ntiles, WG, lds, TF, ahead, xcd_remap, RUNS ? " runs=1" : "", need);
+             ntiles, WG, lds, TF, ahead, xcd_remap, RUNS ? " runs=1" : "", self ? " self=1" : "", need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -283,6 +283,7 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.ahead = ahead;
   p.head = xcd_remap == 1 ? (int)std::min<long long>((long long)k / TF, nfull) : 0;  // head duty: mode 1 only
   p.spin = spin;
+  p.self = self ? 1 : 0;
   p.gran = static_cast<unsigned long long*>(ws.ptr);
   p.runs = reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(ws.ptr) + rec_bytes);
   p.stats = static_cast<unsigned char*>(ws.ptr) + need - trace_bytes - 16;
@@ -316,8 +317,17 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   constexpr bool kRC = sizeof(T) == 4 && C == 1 && !HS;
   constexpr int D = C == 2 ? 768 : 1024;
   int s;
+  // self-published records (AheadParams::self) for fp32 mono windows of at most 3 tiles: no phase A,
+  // the records of the few tiles a window spans are out by the time the scan is done (A/B,
+  // profiles/r03_tuning/self/: k=5000 0.704 -> 0.734, 8192 0.712 -> 0.735, 12288 0.709 -> 0.728;
+  // k=20000 0.712 -> 0.692 and int16 stereo / mono past 3 tiles lose: late neighbours' records)
+#ifdef MAVG_AHEAD_SELF  // tuning builds: 0 never, 1 always (outside the run-total kernel)
+  const bool self = MAVG_AHEAD_SELF != 0;
+#else
+  const bool self = sizeof(T) == 4 && C == 1 && !HS && (long long)k <= 3LL * TF;
+#endif
   if (C == 1 && (long long)k / TF + 1 <= 64)
-    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true, 0, HS, false, WG>(sg, k, st, ws, 512);
+    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true, 0, HS, false, WG>(sg, k, st, ws, 512, self);
 #if !defined(MAVG_AHEAD_FIXED_RUN) && !defined(MAVG_AHEAD_NO_RUNS)
   // run totals (O(J + G) carry items instead of k/T) where the windows are
   // long enough to pay for the kernel's extra registers (4 waves per SIMD
@@ -327,7 +337,7 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS, C <= 2 && U0 == 4 && !HS, WG>(sg, k, st, ws, D);
 #endif
   else
-    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS, false, WG>(sg, k, st, ws, D);
+    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS, false, WG>(sg, k, st, ws, D, self);
   // the Hillis-Steele form also stages the tile: wide frames (e.g. 8 fp32
   // channels, 32 B) take half tiles to stay inside the LDS budget
   if constexpr (HS && U0 > 2) {

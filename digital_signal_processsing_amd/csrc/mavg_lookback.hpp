@@ -208,6 +208,8 @@ struct AheadParams {
   int ahead;        // D (a multiple of 8): block b publishes the records of block b + D's tile
   int head;         // whole tiles a window can span (k / T): the head duty of remap mode 1
   int spin;         // polls of an untagged granule before recomputing it
+  int self;         // self-published records: every tile publishes its own record (no phase A, no
+                    // third read), the carry's records are read after the in-tile scan
   int pre;          // frames in front of `in` that are readable signal (load_elem)
   int eio;          // frame-unit launch on element-aligned pointers (UnitIO::gload)
   unsigned long long* gran;  // [nfull][C][NG] granules, zeroed before the launch
@@ -459,7 +461,7 @@ void ahead_scan_kernel(AheadParams p) {
   const unsigned nb = gridDim.x;
   const unsigned bd = blockIdx.x + (unsigned)p.ahead;  // the block D dispatch slots later (same XCD)
   const long long ja = bd < nb ? map_tile(bd) : -1;
-  const bool produce = ja >= 0 && ja < p.nfull;
+  const bool produce = !p.self && ja >= 0 && ja < p.nfull;
   U_t xa[U];
   if constexpr (WREC) {  // phase A's loads first: the HBM fetch with the longest latency
     if (produce)
@@ -523,7 +525,7 @@ void ahead_scan_kernel(AheadParams p) {
     share(0, ja, r);
   }
   if (tid == 0) MAVG_ATRACE(1, MAVG_ANOW());  // phase A summed (and, WREC, published)
-  const bool own = blockIdx.x < (unsigned)p.ahead && tile < p.nfull;  // no block D slots earlier
+  const bool own = (p.self || blockIdx.x < (unsigned)p.ahead) && tile < p.nfull;  // no block D slots earlier
   if (own) {
     SA r[C];
     wave_record<T, SA, C, F, U>(x, r);
@@ -549,7 +551,7 @@ void ahead_scan_kernel(AheadParams p) {
   {
     MAVG_DCHECK(qhi <= p.nfull * RPT, "record read range", qhi, p.nfull);
     MAVG_DCHECK(!RUNS || (n1 >= 0 && nR >= 0 && rs2 <= qhi && r1 + nR <= p.runs_done), "carry items", n1, nR);
-    if (tid < nitem) {
+    if (!p.self && tid < nitem) {
       item_load(tid, rv);
     } else {
 #pragma unroll
@@ -725,7 +727,7 @@ void ahead_scan_kernel(AheadParams p) {
   for (long long qb = 0; qb < nitem; qb += WG) {
     const long long q = qb + tid;
     const bool act = q < nitem;
-    if (qb != 0) {
+    if (qb != 0 || p.self) {
       if (act) {
         item_load(q, rv);
       } else {

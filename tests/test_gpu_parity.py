@@ -534,6 +534,33 @@ def test_hillis_long_windows_through_the_record_carry(oracle_mod, gpu, C, k, dt)
         assert r["mismatches"] == 0, (algo, r)
 
 
+@pytest.mark.parametrize("k", [4_097, 5_000, 8_191, 8_192, 8_193, 12_288])
+def test_self_published_records(oracle_mod, gpu, k):
+    """fp32 mono windows of at most 3 tiles run the look-ahead scan with
+    self-published records (no phase A; every tile publishes its own record,
+    the carry reads the records after the in-tile scan): every output of
+    rounding data (dist 2) within the bar against the exact window sums,
+    bitwise the same under forced recompute and absent look-ahead, with a
+    ragged tail, and with a history (the window reaching before frame 0)."""
+    import digital_signal_processsing_amd as dsp
+    frames = 3_000_017  # > 700 tiles: ragged XCD runs, head duty, many consumers per record
+    plan = dsp.plan(frames, k, 1, dsp.F32)
+    assert plan.startswith("ahead_scan<") and "self=1" in plan and "wrec=1" in plan, plan
+    assert "self=1" not in dsp.plan(frames, k, 1, dsp.F32, "hillis")
+    x = oracle_mod.synth_f32(frames, seed=91, dist=2)
+    base = _run(x, k, 1, "auto", gpu)
+    for sched in ({"spin": 0}, {"slots": 0}, {"slots": 8, "spin": 0}):
+        y = _with_schedule(sched, lambda: _run(x, k, 1, "auto", gpu))
+        assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), sched
+    r = oracle_mod.check_synth_exact(base, k, 1, seed=91, dist=2, rtol=RTOL)
+    assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, r
+    cut = 2 * k + 777
+    xf = oracle_mod.synth_f32(400_000, offset=k, dist=1)
+    full = oracle_mod.mavg_f32(xf, k, 1)
+    hist = xf[cut - (k - 1): cut].copy()
+    assert_f32_close(_run(xf[cut:], k, 1, "blelloch", gpu, history=hist), full[cut:], f"k={k} history")
+
+
 @pytest.mark.parametrize("fill", [0xFF, "tags"])
 def test_ahead_poisoned_workspace(oracle_mod, gpu, fill):
     """The granules are zeroed on the stream before every launch: a caller

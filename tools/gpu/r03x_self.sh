@@ -1,0 +1,13 @@
+#!/bin/bash
+# self-published records (abl/libmavg_self.so, -DMAVG_AHEAD_SELF=1: no phase A, every tile publishes its own
+# record as soon as its own loads land, the carry's records read after the scan) against the release build
+set -o pipefail
+cd "$(dirname "$0")/../.."
+OUT=gpurun_out/${1:-r03x_self}
+mkdir -p $OUT
+for cfg in "--k 44100 --c 1 --dtype f32" "--k 44100 --c 2 --dtype i16" "--k 44100 --c 1 --dtype i16" "--k 44100 --c 1 --dtype f32 --algo 3" \
+           "--k 20000 --c 1 --dtype f32" "--k 8192 --c 1 --dtype f32" "--k 1000000 --c 1 --dtype f32"; do
+  timeout -k 10 180 python -u tools/tune/ab_libs.py abl/libmavg_cur.so abl/libmavg_self.so \
+     $cfg --rounds 6 --steps 10 >> $OUT/ab.log 2>&1 || { echo "ab failed: $cfg"; exit 1; }
+  tail -4 $OUT/ab.log | head -3 | cut -c1-120
+done
