@@ -49,6 +49,9 @@ WORKLOADS = {
     # a one-second window at 44.1 kHz: too long for an LDS-staged halo, so the
     # one-pass look-ahead scan (the inter-block carry path beyond config #4)
     "long_2p30": (1 << 30, 44100, 1, "f32", "blelloch"),
+    # a window of two tiles past the LDS-staged halo: the look-ahead scan with
+    # self-published records (no phase A)
+    "mid_2p30": (1 << 30, 8192, 1, "f32", "blelloch"),
     # the same one-second window on the reference's int16 PCM path (mono, and
     # stereo as its WAV harness writes it)
     "i16_long": (1 << 30, 44100, 1, "i16", "blelloch"),

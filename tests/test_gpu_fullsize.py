@@ -21,6 +21,7 @@ CONFIGS = [
     ("config3_2p28_k7_direct", 1 << 28, 7, 1, "f32", "direct"),     # configs[2]
     ("config4_2p30_k4096", 1 << 30, 4096, 1, "f32", "blelloch"),    # configs[3]
     ("long_2p30_k44100", 1 << 30, 44100, 1, "f32", "blelloch"),     # look-ahead scan
+    ("mid_2p30_k8192", 1 << 30, 8192, 1, "f32", "blelloch"),        # look-ahead scan, self-published records
     ("hillis_2p30_k1024", 1 << 30, 1024, 1, "f32", "hillis"),
     ("hillis_2p30_k44100", 1 << 30, 44100, 1, "f32", "hillis"),   # Hillis-Steele through the record carry
     ("i16_2p30_k1024", 1 << 30, 1024, 1, "i16", "blelloch"),
