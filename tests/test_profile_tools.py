@@ -52,10 +52,15 @@ def test_traffic_json_covers_every_workload():
     for key, v in t.items():
         name = key.split(":")[0]
         n, k, C, dt, algo = bench.WORKLOADS[name]
-        if k * C * (4 if dt == "f32" else 2) > (2 << 20):
-            # windows reaching past what an XCD's 4 MB L2 still holds of the
-            # stream: every x[n-k] is fetched again from beyond L2 (MALL or
-            # HBM): one extra read of the input, ~1.5x (very long windows)
+        wb = k * C * (4 if dt == "f32" else 2)
+        if wb > (8 << 20):
+            # an XCD's share of the window (2 MB at k=4e6 fp32) plus the
+            # look-ahead prefetch no longer fit its 4 MB L2: x[n-k] is fetched
+            # again from beyond L2 (MALL or HBM), ~1.5x (very long windows)
             assert 1.3 < v["traffic_over_algorithmic"] < 1.55, (key, v)
+        elif wb > (2 << 20):
+            # window-matched XCD runs keep most x[n-k] on the tile's own XCD
+            # (k=1e6 fp32: 1.11x, r03x; one run per XCD measured 1.49x)
+            assert 0.99 < v["traffic_over_algorithmic"] < 1.25, (key, v)
         else:
             assert 0.99 < v["traffic_over_algorithmic"] < 1.05, (key, v)

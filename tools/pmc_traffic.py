@@ -56,7 +56,8 @@ def plan_key(plan):
         args = (T, acc, kv["C"], kv["F"], kv["U"], wg, kv.get("nt", "0"))
     elif fam == "ahead_scan":
         b = {"0": "false", "1": "true"}
-        args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], b[kv["rc"]], b[kv["dma"]], b[kv["wrec"]], kv["dv"], hs)
+        args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], b[kv["rc"]], b[kv["dma"]], b[kv["wrec"]], kv["dv"], hs,
+                "true" if " runs=1" in plan else "false", wg)
     else:
         args = (T, acc)
     return FAMILY[fam], args
