@@ -388,6 +388,14 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
     if (wg == 512 && fits(2, 512)) return launch_tile_scan<T, A, C, F, 2, HS, kNtS, 512, kR>(sg, k, st);
     if (wg == 1024 && fits(2, 1024)) return launch_tile_scan<T, A, C, F, 2, HS, kNtS, 1024, kR>(sg, k, st);
   }
+  if constexpr (!HS && sizeof(T) == 4 && C == 4 && F == 2) {
+    // fp32 4 channels in 32-B units (dispatch_scan_c): 1024-frame tiles up to
+    // 4 KiB of halo, then the look-ahead scan in 1024-frame tiles (in-process
+    // A/B against 1-frame units, profiles/r03_tuning/c4/: k=7 0.46 -> 0.64,
+    // k=200 0.45 -> 0.65, k=2000 0.41 -> 0.50, k=44100 0.40 -> 0.48)
+    if (halo_bytes <= 4096 && fits(2, kWG)) return launch_tile_scan<T, A, C, F, 2, false, kNtS, kWG, true>(sg, k, st);
+    return dispatch_ahead<T, A, C, F, false, 2>(sg, k, st, ws);
+  }
   if constexpr (!HS) {
     // RC (in-lane prefix rebuilt after the barrier): on for fp32, off for
     // int16 (measured both ways, tools/tune/ab_rc.sh, sweep_lookback2.sh).
@@ -460,6 +468,11 @@ int dispatch_scan_c(bool vec, bool hs, const Sig& sg, int k, int block, hipStrea
   constexpr int VF = (C * (int)sizeof(T) <= 16 && 16 % (C * (int)sizeof(T)) == 0) ? 16 / (C * (int)sizeof(T)) : 0;
   if constexpr (VF > 0) {
     if (vec) {
+      // fp32 with 4 channels: a frame is one 16-B unit, so every unit costs 4
+      // fp64 wave scans; the Blelloch flavour takes 2 frames (32 B) per lane
+      if constexpr (sizeof(T) == 4 && C == 4) {
+        if (!hs && !sg.eio) return dispatch_scan_f<T, A, C, 2, false>(sg, k, block, st, ws);
+      }
       return hs ? dispatch_scan_f<T, A, C, VF, true>(sg, k, block, st, ws)
                 : dispatch_scan_f<T, A, C, VF, false>(sg, k, block, st, ws);
     }

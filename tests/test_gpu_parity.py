@@ -333,7 +333,7 @@ def _lookback_tile(dsp, n, k, C, dt):
     return int(plan.split("tile_frames=")[1].split()[0])
 
 
-@pytest.mark.parametrize("C", [1, 2, 3, 8])
+@pytest.mark.parametrize("C", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("dtype", ["i16", "f32"])
 def test_ahead_window_edges(oracle_mod, gpu, C, dtype):
     """k just below / at / above multiples of the tile (empty, one-frame and
@@ -559,6 +559,29 @@ def test_self_published_records(oracle_mod, gpu, k):
     full = oracle_mod.mavg_f32(xf, k, 1)
     hist = xf[cut - (k - 1): cut].copy()
     assert_f32_close(_run(xf[cut:], k, 1, "blelloch", gpu, history=hist), full[cut:], f"k={k} history")
+
+
+@pytest.mark.parametrize("k", [1, 7, 64, 256, 257, 500, 1001, 2000, 44_100])
+def test_f32_four_channels_in_wide_units(oracle_mod, gpu, k):
+    """fp32 with 4 channels runs the Blelloch flavour in 32-B units (two
+    frames per lane): the tile scan up to 4 KiB of halo, the look-ahead scan
+    past it, also for windows shorter than its 1024-frame tile; rounding data
+    against the oracle, a view 16 B into an allocation (16-B but not 32-B
+    aligned), and the frame-unit form (blelloch_scalar) for comparison."""
+    import digital_signal_processsing_amd as dsp
+    import torch
+    C, frames = 4, 300_007
+    plan = dsp.plan(frames * C, k, C, dsp.F32)
+    assert ",C=4,F=2," in plan, plan
+    x = oracle_mod.synth_f32(frames * C, offset=k, dist=1)
+    ref = oracle_mod.mavg_f32(x, k, C)
+    assert_f32_close(_run(x, k, C, "blelloch", gpu), ref, f"k={k}")
+    xb = torch.zeros(frames * C + 4, dtype=torch.float32, device=gpu)
+    xb[4:] = torch.from_numpy(x).to(gpu)
+    yb = torch.zeros_like(xb)
+    dsp.moving_average_into(xb[4:], yb[4:], k, C, "blelloch")
+    assert_f32_close(yb[4:].cpu().numpy(), ref, f"k={k} 16-B view")
+    assert_f32_close(_run(x, k, C, "blelloch_scalar", gpu), ref, f"k={k} scalar")
 
 
 @pytest.mark.parametrize("fill", [0xFF, "tags"])
