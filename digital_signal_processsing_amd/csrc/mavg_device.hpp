@@ -147,10 +147,12 @@ struct Unit {
   T e[VE];
 };
 
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 template <int BYTES> struct RawVec;
+template <> struct RawVec<64> { using type = u32x16; };  // 2 frames of 8 fp32 channels (4 x 16-B accesses)
 template <> struct RawVec<32> { using type = u32x8; };
 template <> struct RawVec<16> { using type = u32x4; };
 template <> struct RawVec<8> { using type = u32x2; };
@@ -160,7 +162,7 @@ template <> struct RawVec<2> { using type = uint16_t; };
 template <typename T, int VE>
 struct UnitIO {
   static constexpr int kBytes = VE * (int)sizeof(T);
-  static constexpr bool kVec = (kBytes == 32 || kBytes == 16 || kBytes == 8 || kBytes == 4 || kBytes == 2);
+  static constexpr bool kVec = (kBytes == 64 || kBytes == 32 || kBytes == 16 || kBytes == 8 || kBytes == 4 || kBytes == 2);
 
   // p is aligned to kBytes when kVec (checked on the host for the base pointer).
   // NT: non-temporal hint (streamed-once HBM data; never used on LDS).

@@ -396,6 +396,12 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
     if (halo_bytes <= 4096 && fits(2, kWG)) return launch_tile_scan<T, A, C, F, 2, false, kNtS, kWG, true>(sg, k, st);
     return dispatch_ahead<T, A, C, F, false, 2>(sg, k, st, ws);
   }
+  if constexpr (!HS && sizeof(T) == 4 && C == 8 && F == 2) {
+    // fp32 8 channels in 64-B units (2 frames per lane, 4 x 16-B accesses), past
+    // the LDS-staged halo only (dispatch_scan_c): the look-ahead scan in 512-frame
+    // tiles (profiles/r03_tuning/c8/: k=1024 0.199 -> 0.253, k=44100 0.181 -> 0.212)
+    return dispatch_ahead<T, A, C, F, false, 1>(sg, k, st, ws);
+  }
   if constexpr (!HS) {
     // RC (in-lane prefix rebuilt after the barrier): on for fp32, off for
     // int16 (measured both ways, tools/tune/ab_rc.sh, sweep_lookback2.sh).
@@ -466,6 +472,14 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
 template <typename T, typename A, int C>
 int dispatch_scan_c(bool vec, bool hs, const Sig& sg, int k, int block, hipStream_t st, Workspace ws) {
   constexpr int VF = (C * (int)sizeof(T) <= 16 && 16 % (C * (int)sizeof(T)) == 0) ? 16 / (C * (int)sizeof(T)) : 0;
+  // fp32 with 8 channels (32-B frames, no vector form): past the 1-frame
+  // tiles' LDS-staged halo (8 KiB, k > 256) the look-ahead scan takes 2 frames
+  // per lane as well; below it the 1-frame tiles stay (the 64-B-unit tile
+  // spills: k=7 0.416 -> 0.383)
+  if constexpr (sizeof(T) == 4 && C == 8) {
+    if (vec && !hs && !sg.eio && block == 0 && (long long)k * C * (long long)sizeof(T) > 8192)
+      return dispatch_scan_f<T, A, C, 2, false>(sg, k, block, st, ws);
+  }
   if constexpr (VF > 0) {
     if (vec) {
       // fp32 with 4 channels: a frame is one 16-B unit, so every unit costs 4

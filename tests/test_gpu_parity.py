@@ -561,18 +561,20 @@ def test_self_published_records(oracle_mod, gpu, k):
     assert_f32_close(_run(xf[cut:], k, 1, "blelloch", gpu, history=hist), full[cut:], f"k={k} history")
 
 
-@pytest.mark.parametrize("k", [1, 7, 64, 256, 257, 500, 1001, 2000, 44_100])
-def test_f32_four_channels_in_wide_units(oracle_mod, gpu, k):
+@pytest.mark.parametrize("C,k", [(4, 1), (4, 7), (4, 64), (4, 256), (4, 257), (4, 500), (4, 1001), (4, 2000),
+                                 (4, 44_100), (8, 7), (8, 256), (8, 257), (8, 1024), (8, 44_100)])
+def test_f32_four_channels_in_wide_units(oracle_mod, gpu, C, k):
     """fp32 with 4 channels runs the Blelloch flavour in 32-B units (two
     frames per lane): the tile scan up to 4 KiB of halo, the look-ahead scan
-    past it, also for windows shorter than its 1024-frame tile; rounding data
+    past it, also for windows shorter than its 1024-frame tile; with 8
+    channels the look-ahead scan (k > 256) takes 64-B units.  Rounding data
     against the oracle, a view 16 B into an allocation (16-B but not 32-B
     aligned), and the frame-unit form (blelloch_scalar) for comparison."""
     import digital_signal_processsing_amd as dsp
     import torch
-    C, frames = 4, 300_007
+    frames = 300_007
     plan = dsp.plan(frames * C, k, C, dsp.F32)
-    assert ",C=4,F=2," in plan, plan
+    assert (f",C={C},F=2," in plan) == (C == 4 or k > 256), plan
     x = oracle_mod.synth_f32(frames * C, offset=k, dist=1)
     ref = oracle_mod.mavg_f32(x, k, C)
     assert_f32_close(_run(x, k, C, "blelloch", gpu), ref, f"k={k}")
