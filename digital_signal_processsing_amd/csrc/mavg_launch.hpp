@@ -399,7 +399,7 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
   if constexpr (!HS && sizeof(T) == 4 && C == 8 && F == 2) {
     // fp32 8 channels in 64-B units (2 frames per lane, 4 x 16-B accesses), past
     // the LDS-staged halo only (dispatch_scan_c): the look-ahead scan in 512-frame
-    // tiles (profiles/r03_tuning/c8/: k=1024 0.199 -> 0.253, k=44100 0.181 -> 0.212)
+    // tiles (profiles/r03_tuning/c8/: k=300 0.208 -> 0.267, k=1024 0.198 -> 0.238, k=44100 0.180 -> 0.208)
     return dispatch_ahead<T, A, C, F, false, 1>(sg, k, st, ws);
   }
   if constexpr (!HS) {
