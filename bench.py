@@ -61,6 +61,11 @@ WORKLOADS = {
     "hillis_long": (1 << 30, 44100, 1, "f32", "hillis"),
     "long_1m": (1 << 30, 1_000_000, 1, "f32", "blelloch"),
     "long_4m": (1 << 30, 4_000_000, 1, "f32", "blelloch"),
+    # fp32 multi-channel frames: stereo (the fp32 form of the reference's WAV
+    # harness layout and of its only vectorized scan, longlong2 frames), 4 and 8
+    "f32_stereo_2p30": (1 << 30, 1024, 2, "f32", "blelloch"),
+    "f32_c4_2p30": (1 << 30, 1024, 4, "f32", "blelloch"),
+    "f32_c8_2p30": (1 << 30, 1024, 8, "f32", "blelloch"),
 }
 
 
@@ -344,6 +349,51 @@ def shard_timing(args, x, y, k, C, algo, ev, hev, value, n, rank, world):
     }
 
 
+def device_record(rank: int) -> dict:
+    """This rank's device as the communicator sees it (N > 1 `rccl` block)."""
+    import torch
+    dev = torch.cuda.current_device()
+    pr = torch.cuda.get_device_properties(dev)
+    return {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": dev,
+            "pci_bus_id": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}",
+            "uuid": str(pr.uuid), "name": pr.name, "host": socket.gethostname(),
+            "visible_devices": torch.cuda.device_count()}
+
+
+def rccl_block(every: list, backend: str, version, halo_bytes: int, world: int) -> dict:
+    """The N > 1 line's `rccl` block: what the communicator saw -- its world
+    size and backend, the RCCL version torch links, each rank's device (index,
+    PCI bus id, UUID, host) and the halo bytes each exchange moves.  Under
+    backend "nccl" (= RCCL) the N ranks must hold N distinct devices, or the
+    run fails loudly (a scaling record that shares GPUs is not one); the gloo
+    rehearsal may share a device and says so."""
+    keys = {(r["host"], r["uuid"]) for r in every}
+    distinct = len(keys) == len(every) == world
+    if backend == "nccl" and not distinct:
+        raise SystemExit(f"RCCL world of {world} ranks on {len(keys)} distinct devices: {every}")
+    return {
+        "world_size": world,
+        "backend": backend,
+        "rccl_version": version,
+        "devices": every,
+        "distinct_devices": distinct,
+        "halo_bytes": halo_bytes,
+        "exchange": "batch_isend_irecv: (k-1)*C samples from rank r to rank r+1, once per step",
+    }
+
+
+def comm_report(rank: int, world: int, halo_bytes: int) -> dict:
+    import torch
+    import torch.distributed as dist
+    every = [None] * world
+    dist.all_gather_object(every, device_record(rank))
+    try:
+        version = ".".join(str(v) for v in torch.cuda.nccl.version())
+    except Exception:  # noqa: BLE001 - a build without RCCL: report it as absent
+        version = None
+    return rccl_block(every, dist.get_backend(), version, halo_bytes, dist.get_world_size())
+
+
 def run_workload(args, name, rank, world, with_cpu):
     import torch
     import digital_signal_processsing_amd as dsp
@@ -461,6 +511,8 @@ def run_workload(args, name, rank, world, with_cpu):
             res = {"ranks": world, "slices": sum(r["slices"] for r in allres),
                    "mismatches": sum(r["mismatches"] for r in allres)}
         line["check"] = res
+    if world > 1:
+        line["rccl"] = comm_report(rank, world, (k - 1) * C * elem)
     if world > 1:  # after --check: the single launches overwrite the output with a no-halo result
         line["scaling_detail"] = shard_timing(args, x, y, k, C, algo, ev, hev, value, n, rank, world)
     # same-box streaming ceiling: the library's flat non-temporal copy over the

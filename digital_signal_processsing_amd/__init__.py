@@ -74,10 +74,10 @@ def _stream_handle(stream, device) -> int:
 
 
 def workspace_bytes(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto",
-                    block_size: int = 0) -> int:
+                    block_size: int = 0, library: Optional[str] = None) -> int:
     import ctypes
     out = ctypes.c_size_t(0)
-    _lib.check(_lib.load().mavg_workspace_bytes(n, channels, grade, dtype, _algo_code(algo), block_size,
+    _lib.check(_lib.load(library).mavg_workspace_bytes(n, channels, grade, dtype, _algo_code(algo), block_size,
                                                 ctypes.byref(out)), "mavg_workspace_bytes")
     return out.value
 
@@ -86,23 +86,26 @@ def resolve_algo(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="
     return algo_name(_lib.load().mavg_resolve_algo(n, channels, grade, dtype, _algo_code(algo)))
 
 
-def plan(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto", block_size: int = 0) -> str:
+def plan(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto", block_size: int = 0,
+         library: Optional[str] = None) -> str:
     """The kernel and launch geometry mavg_run would use (nothing is launched)."""
     import ctypes
     buf = ctypes.create_string_buffer(256)
-    _lib.check(_lib.load().mavg_plan(n, channels, grade, dtype, _algo_code(algo), block_size, buf, len(buf)),
+    _lib.check(_lib.load(library).mavg_plan(n, channels, grade, dtype, _algo_code(algo), block_size, buf, len(buf)),
                "mavg_plan")
     return buf.value.decode()
 
 
 def moving_average_into(x, out, grade: int, channels: int = 1, algo="auto", history=None,
-                        block_size: int = 0, stream=None, workspace=None) -> None:
+                        block_size: int = 0, stream=None, workspace=None, library: Optional[str] = None) -> None:
     """Enqueue ``out = moving_average(x)`` on ``stream`` (default: current).
 
     ``workspace``: optional caller-owned device buffer (any dtype, contiguous)
     of at least ``workspace_bytes(...)`` bytes, like the reference's
     ``DspWorkspace`` scratch; without it the look-back scan (long windows)
-    takes one from torch's caching allocator per call."""
+    takes one from torch's caching allocator per call.
+    ``library``: path of another build of the same ABI (the debug build,
+    ``_lib.DEBUG_LIB_PATH``); default the release ``libmavg.so``."""
     torch = _torch()
     if not (x.is_cuda and out.is_cuda):
         raise ValueError("x and out must be device tensors (libmavg has no CPU path)")
@@ -120,7 +123,7 @@ def moving_average_into(x, out, grade: int, channels: int = 1, algo="auto", hist
         hist_ptr = history.data_ptr() if history.numel() else None
     # workspace (look-back scan only): from torch's caching allocator, tied to
     # the launch stream so it is not handed out again before the kernel ends
-    ws_n = workspace_bytes(x.numel(), grade, channels, dt, algo, block_size)
+    ws_n = workspace_bytes(x.numel(), grade, channels, dt, algo, block_size, library)
     ws = None
     if ws_n and workspace is not None:
         if not (workspace.is_cuda and workspace.is_contiguous()):
@@ -141,7 +144,7 @@ def moving_average_into(x, out, grade: int, channels: int = 1, algo="auto", hist
         # there, and record_stream only protects the free)
         with torch.cuda.stream(stream) if stream is not None else _nullctx():
             ws = torch.empty(ws_n, dtype=torch.uint8, device=x.device)
-    st = _lib.load().mavg_run(x.data_ptr(), out.data_ptr(), x.numel(), channels, grade, dt,
+    st = _lib.load(library).mavg_run(x.data_ptr(), out.data_ptr(), x.numel(), channels, grade, dt,
                               _algo_code(algo), block_size, hist_ptr,
                               ws.data_ptr() if ws is not None else None, ws_n,
                               _stream_handle(stream, x.device))
@@ -149,7 +152,7 @@ def moving_average_into(x, out, grade: int, channels: int = 1, algo="auto", hist
 
 
 def moving_average(x, grade: int, channels: int = 1, algo="auto", history=None,
-                   block_size: int = 0, stream=None):
+                   block_size: int = 0, stream=None, library: Optional[str] = None):
     """Causal ``grade``-frame moving average of an interleaved signal ``x``."""
     torch = _torch()
     if stream is not None and stream != torch.cuda.current_stream(x.device):
@@ -158,7 +161,7 @@ def moving_average(x, grade: int, channels: int = 1, algo="auto", history=None,
         stream.wait_stream(torch.cuda.current_stream(x.device))
         with torch.cuda.stream(stream):
             out = torch.empty_like(x)
-        moving_average_into(x, out, grade, channels, algo, history, block_size, stream)
+        moving_average_into(x, out, grade, channels, algo, history, block_size, stream, library=library)
         # the kernel reads x and history on `stream`: keep the caching
         # allocator from handing their blocks out again before it ends
         x.record_stream(stream)
@@ -166,7 +169,7 @@ def moving_average(x, grade: int, channels: int = 1, algo="auto", history=None,
             history.record_stream(stream)
         return out
     out = torch.empty_like(x)
-    moving_average_into(x, out, grade, channels, algo, history, block_size, stream)
+    moving_average_into(x, out, grade, channels, algo, history, block_size, stream, library=library)
     return out
 
 

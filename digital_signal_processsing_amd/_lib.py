@@ -60,8 +60,11 @@ EXPORTED_SYMBOLS = (
     "mavg_strerror",
     "mavg_algo_name",
     "mavg_abi_version",
-    "mavg_test_ahead_schedule",
 )
+# exported by the debug build only (include/mavg_debug.h)
+DEBUG_SYMBOLS = ("mavg_test_ahead_schedule",)
+ABI_VERSION = 3
+DEBUG_LIB_PATH = os.path.join(_PKG, "lib", "libmavg_debug.so")
 
 
 class MavgLibraryError(RuntimeError):
@@ -74,21 +77,25 @@ class MavgError(RuntimeError):
         super().__init__(f"{what}: {strerror(status)} (status {status})")
 
 
-_lib = None
+_libs = {}
 
 
-def load() -> ctypes.CDLL:
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+def load(path: str = None) -> ctypes.CDLL:
+    """The library at `path` (default: LIB_PATH, the release build unless
+    MAVG_LIBRARY names another), loaded once per path.  Each path is its own
+    RTLD_LOCAL handle, so the tests can drive the debug build
+    (DEBUG_LIB_PATH) beside the release one in one process."""
+    path = path or LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
         raise MavgLibraryError(
-            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(hipcc --offload-arch=gfx950); there is no CPU fallback")
     try:
-        lib = ctypes.CDLL(LIB_PATH)
+        lib = ctypes.CDLL(path, mode=os.RTLD_LOCAL | os.RTLD_NOW)
     except OSError as e:  # pragma: no cover - depends on the runtime image
-        raise MavgLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+        raise MavgLibraryError(f"failed to load {path}: {e}") from e
     vp, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
     lib.mavg_workspace_bytes.argtypes = [sz, i, i, i, i, i, ctypes.POINTER(sz)]
     lib.mavg_workspace_bytes.restype = i
@@ -106,11 +113,12 @@ def load() -> ctypes.CDLL:
     lib.mavg_algo_name.restype = ctypes.c_char_p
     lib.mavg_stream_copy.argtypes = [vp, vp, sz, vp]
     lib.mavg_stream_copy.restype = i
-    lib.mavg_test_ahead_schedule.argtypes = [i, i]
-    lib.mavg_test_ahead_schedule.restype = i
+    if hasattr(lib, "mavg_test_ahead_schedule"):  # debug build only
+        lib.mavg_test_ahead_schedule.argtypes = [i, i]
+        lib.mavg_test_ahead_schedule.restype = i
     lib.mavg_abi_version.argtypes = []
     lib.mavg_abi_version.restype = i
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 

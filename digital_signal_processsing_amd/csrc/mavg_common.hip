@@ -5,8 +5,10 @@
 namespace mavg {
 
 thread_local LaunchPlan* g_plan = nullptr;
+#ifdef MAVG_TEST_HOOKS
 std::atomic<int> g_test_ahead_slots{-1};
 std::atomic<int> g_test_ahead_spin{-1};
+#endif
 
 // ---- per-device attribute cache (no stream work, capture-safe) --------------
 static std::atomic<int> g_cu_count[kMaxDevices];
@@ -39,8 +41,11 @@ OutParams make_out_params(int k) {
 
 }  // namespace mavg
 
+#ifdef MAVG_TEST_HOOKS
+// include/mavg_debug.h: exported by the debug build (lib/libmavg_debug.so) only
 extern "C" int mavg_test_ahead_schedule(int slots, int spin) {
   mavg::g_test_ahead_slots.store(slots < 0 ? -1 : std::min(slots, 1 << 30), std::memory_order_relaxed);
   mavg::g_test_ahead_spin.store(spin < 0 ? -1 : std::min(spin, 1 << 20), std::memory_order_relaxed);
   return MAVG_OK;
 }
+#endif

@@ -6,7 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Debug build (make DEBUG=1 -> libmavg_debug.so): device bounds checks on LDS
+// Debug build (make -C csrc debug -> libmavg_debug.so): device bounds checks on LDS
 // stage indices, x[n-k] extractions, tile indices and record slots; a failed
 // check prints (what, block, thread, two values) and traps.  Compiled out of
 // the release library.

@@ -153,12 +153,16 @@ int launch_tile_scan(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
 // Workspace: the granule block, at the start of the workspace, padded to
 // 16 bytes (the memset's fast form, cdna_hip_programming.md Guideline 16).
 constexpr int kAheadSpin = 256;   // polls of an untagged granule before recomputing it
-// Test hook (mavg_test_ahead_schedule): the parity tests force the
+// Test hook (mavg_test_ahead_schedule, include/mavg_debug.h; compiled into
+// the debug build only, MAVG_TEST_HOOKS): the parity tests force the
 // recompute path with spin 0 and short or absent look-ahead; results are
 // bitwise the same for every setting.  -1 = the tuned defaults.  Relaxed
-// atomics: no environment reads on the launch path.
+// atomics: no environment reads on the launch path.  The release library has
+// no process-wide mutable state.
+#ifdef MAVG_TEST_HOOKS
 extern std::atomic<int> g_test_ahead_slots;
 extern std::atomic<int> g_test_ahead_spin;
+#endif
 template <typename T, typename A, int C, int F, int U>
 constexpr size_t ahead_granule_bytes(long long nrec) {
   using SA = typename ScanAcc<T, A>::type;
@@ -202,16 +206,22 @@ template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA
 int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead, bool self = false) {
   constexpr int NW = WG / 64;
   const long long nframes = sg.nframes;
+  ahead &= ~7;
+  // the tuned D sets the run length G below; the test hook changes only the
+  // producer distance, so a forced schedule keeps the plan's tile -> XCD
+  // mapping and run-total grouping (the same decomposition, the same bits)
+  const int ahead_plan = ahead;
+  int spin = kAheadSpin;
+#ifdef MAVG_TEST_HOOKS
   {
     const int t = g_test_ahead_slots.load(std::memory_order_relaxed);
-    if (t >= 0) ahead = t;
-    ahead &= ~7;
+    if (t >= 0) ahead = t & ~7;
   }
-  int spin = kAheadSpin;
   {
     const int t = g_test_ahead_spin.load(std::memory_order_relaxed);
     if (t >= 0) spin = t;
   }
+#endif
   // one contiguous run per XCD (remap mode 1: x[n-k] is then an L2 hit of the
   // same XCD) while the window's bytes fit comfortably in an XCD's 4 MB L2;
   // past that, 8 separate runs would fetch x[n-k] from the MALL: window-
@@ -224,7 +234,7 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   const int xcd_remap = ahead_past_l2(k, C, sizeof(T), TF) ? MAVG_AHEAD_FIXED_RUN : 1;
   static_assert(!RUNS, "run totals need window-matched runs");
 #else
-  const int xcd_remap = ahead_past_l2(k, C, sizeof(T), TF) ? ahead_run_length(k, TF, ahead) : 1;
+  const int xcd_remap = ahead_past_l2(k, C, sizeof(T), TF) ? ahead_run_length(k, TF, ahead_plan) : 1;
   if (RUNS && xcd_remap == 1) return MAVG_ERR_UNSUPPORTED;
 #endif
   constexpr int VE = F * C;

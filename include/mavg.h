@@ -38,8 +38,9 @@
  * reference scans in place; this library does not).  Thread-safe and
  * re-entrant; the only process state is per DEVICE (keyed on hipGetDevice):
  * the CU count and, per kernel, whether its dynamic-LDS limit has been raised
- * on that device -- so one process may drive several devices -- plus the
- * process-wide test hook mavg_test_ahead_schedule.
+ * on that device -- so one process may drive several devices.  (The test
+ * hook that forces the look-ahead scan's schedule is process-wide state; it
+ * lives in the debug build only, include/mavg_debug.h.)
  */
 #ifndef MAVG_H
 #define MAVG_H
@@ -51,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MAVG_ABI_VERSION 2  /* 2: mavg_plan takes block_size; mavg_test_ahead_schedule */
+#define MAVG_ABI_VERSION 3  /* 2: mavg_plan takes block_size; 3: the schedule test hook moved to mavg_debug.h */
 
 typedef enum {
     MAVG_I16 = 0, /* int16 PCM in/out (the reference's WAV data path) */
@@ -142,14 +143,6 @@ int mavg_fill_synthetic(void* d_out, size_t n_samples, int dtype, uint64_t seed,
  * read against the same box's achievable streaming rate.  bytes a multiple
  * of 16, both pointers 16-B aligned. */
 int mavg_stream_copy(const void* d_in, void* d_out, size_t bytes, void* stream);
-
-/* TEST HOOK (parity tests only): override the look-ahead scan's schedule --
- * `slots` dispatch slots between a record's producer and its consumers
- * (default 512), `spin` polls of an unpublished record before the consumer
- * recomputes it (default 256); a negative value restores the default.
- * Outputs are bitwise identical for every setting; only the path that
- * produces a record changes.  Process-wide; returns MAVG_OK. */
-int mavg_test_ahead_schedule(int slots, int spin);
 
 const char* mavg_strerror(int status);
 const char* mavg_algo_name(int algo);

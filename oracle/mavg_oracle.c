@@ -296,13 +296,18 @@ static inline int fx64(float x, __int128* out)
     *out = (u >> 31) ? -v : v;
     return 0;
 }
-/* (double) of an __int128 without the library call: two exact halves, one
- * rounding each (relative error < 2^-52) */
+/* (double) of an __int128 without the library call: the magnitude's two
+ * halves, one rounding each, then the sum (relative error < 2^-51 for either
+ * sign) */
 static inline double i128_to_double(__int128 s)
 {
-    const int64_t hi = (int64_t)(s >> 64);
-    const uint64_t lo = (uint64_t)s;
-    return (double)hi * 0x1p64 + (double)lo;
+    /* magnitude first, then the sign: (double)hi * 2^64 + (double)lo with a
+     * negative hi cancels catastrophically for small |s| (s = -5: hi = -1,
+     * lo = 2^64 - 5 rounds to 2^64, the sum to 0) */
+    const int neg = s < 0;
+    const unsigned __int128 u = neg ? -(unsigned __int128)s : (unsigned __int128)s;
+    const double d = (double)(uint64_t)(u >> 64) * 0x1p64 + (double)(uint64_t)u;
+    return neg ? -d : d;
 }
 
 int oracle_check_synth_f32_exact(const float* y, size_t n, int C, int k, uint64_t seed, uint64_t offset,

@@ -11,20 +11,34 @@ from digital_signal_processsing_amd import _lib
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _header_symbols():
-    text = open(os.path.join(ROOT, "include", "mavg.h")).read()
+def _header_symbols(header="mavg.h"):
+    text = open(os.path.join(ROOT, "include", header)).read()
     return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(mavg_\w+)\s*\(", text, re.M)))
 
 
 def test_header_and_binding_agree():
     assert _header_symbols() == sorted(_lib.EXPORTED_SYMBOLS)
+    assert _header_symbols("mavg_debug.h") == sorted(_lib.DEBUG_SYMBOLS)
 
 
 def test_library_exports_every_symbol():
     lib = _lib.load()
     for name in _header_symbols():
         assert hasattr(lib, name), name
-    assert lib.mavg_abi_version() == 2
+    assert lib.mavg_abi_version() == _lib.ABI_VERSION == 3
+
+
+def test_release_library_has_no_test_hook():
+    """The schedule test hook (process-wide state) is exported by the debug
+    build only (include/mavg_debug.h); the release build exports exactly
+    include/mavg.h."""
+    lib = _lib.load()
+    for name in _lib.DEBUG_SYMBOLS:
+        assert not hasattr(lib, name), name
+    dbg = _lib.load(_lib.DEBUG_LIB_PATH)
+    for name in _header_symbols() + _header_symbols("mavg_debug.h"):
+        assert hasattr(dbg, name), name
+    assert dbg.mavg_abi_version() == _lib.ABI_VERSION
 
 
 def test_strerror_and_names():
@@ -94,7 +108,7 @@ def test_fill_synthetic_validates():
 
 
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):
-    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "_libs", {})
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_lib.MavgLibraryError):
         _lib.load()

@@ -73,3 +73,25 @@ def test_bench_self_launch_two_ranks_gloo_check(gpu):
     assert [r["rank"] for r in sd["per_rank"]] == [0, 1]
     for r in sd["per_rank"]:
         assert r["halo_wait_ms"] >= 0 and r["head_ms"] > 0 and r["single_launch_gsamples_s"] > 0, r
+    rc = d["rccl"]  # what the communicator saw (gloo rehearsal: both ranks may share GPU 0)
+    assert rc["world_size"] == 2 and rc["backend"] == "gloo" and rc["halo_bytes"] == 1023 * 4, rc
+    assert [r["rank"] for r in rc["devices"]] == [0, 1] and all(r["pci_bus_id"] for r in rc["devices"]), rc
+    assert rc["distinct_devices"] == (len({r["uuid"] for r in rc["devices"]}) == 2), rc
+
+
+def _rec(rank, uuid, host="h"):
+    return {"rank": rank, "device": rank, "pci_bus_id": f"0000:{rank:02x}:00", "uuid": uuid, "host": host}
+
+
+def test_rccl_block_requires_distinct_devices_under_nccl():
+    """The N > 1 JSON line's `rccl` block proves by itself that N ranks held N
+    devices: under nccl (RCCL) a shared device fails the run; gloo may share."""
+    import bench
+    ok = bench.rccl_block([_rec(0, "a"), _rec(1, "b")], "nccl", "2.27.7", 4092, 2)
+    assert ok["distinct_devices"] and ok["world_size"] == 2 and ok["halo_bytes"] == 4092
+    assert ok["rccl_version"] == "2.27.7" and [r["rank"] for r in ok["devices"]] == [0, 1]
+    with pytest.raises(SystemExit, match="distinct devices"):
+        bench.rccl_block([_rec(0, "a"), _rec(1, "a")], "nccl", "2.27.7", 4092, 2)
+    assert not bench.rccl_block([_rec(0, "a"), _rec(1, "a")], "gloo", None, 4092, 2)["distinct_devices"]
+    # the same UUID string on two hosts is two devices
+    assert bench.rccl_block([_rec(0, "a", "h0"), _rec(1, "a", "h1")], "nccl", None, 8, 2)["distinct_devices"]

@@ -21,11 +21,11 @@ def _dev(x, gpu):
     return torch.from_numpy(np.ascontiguousarray(x)).to(gpu)
 
 
-def _run(x_np, k, C, algo, gpu, history=None):
+def _run(x_np, k, C, algo, gpu, history=None, library=None):
     import digital_signal_processsing_amd as dsp
     x = _dev(x_np, gpu)
     h = _dev(history, gpu) if history is not None else None
-    y = dsp.moving_average(x, k, channels=C, algo=algo, history=h)
+    y = dsp.moving_average(x, k, channels=C, algo=algo, history=h, library=library)
     return y.cpu().numpy()
 
 
@@ -299,8 +299,11 @@ def test_period_remap_very_long_windows_with_tail(oracle_mod, gpu, dtype, C, k, 
         x = oracle_mod.synth_i16(frames * C, offset=77)
         base = _run(x, k, C, algo, gpu)
         assert np.array_equal(base, oracle_mod.mavg_i16(x, k, C)), plan
-    for sched in ({"spin": 0}, {"slots": 0}, {"slots": 8, "spin": 0}):
-        y = _with_schedule(sched, lambda: _run(x, k, C, algo, gpu))
+    for sched in ({}, {"spin": 0}, {"slots": 0}, {"slots": 8, "spin": 0}):
+        # the forced schedule keeps the plan's runs (G) and run-total grouping
+        p = _with_schedule(sched, lambda lib: dsp.plan(frames * C, k, C, code, algo, library=lib))
+        assert int(p.split("remap=")[1].split()[0]) == G and ("runs=1" in p) == ("runs=1" in plan), (sched, p)
+        y = _with_schedule(sched, lambda lib: _run(x, k, C, algo, gpu, library=lib))
         assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), sched
 
 
@@ -462,12 +465,15 @@ def test_ahead_large_stereo_slices(oracle_mod, gpu):
 
 
 def _with_schedule(sched, fn):
-    """Run fn under a forced look-ahead schedule (mavg_test_ahead_schedule)."""
+    """fn(library) under a forced look-ahead schedule: the schedule hook
+    (mavg_test_ahead_schedule, include/mavg_debug.h) is exported by the debug
+    build only, so fn runs on lib/libmavg_debug.so; the callers compare its
+    output bitwise with the release build's default schedule."""
     from digital_signal_processsing_amd import _lib
-    lib = _lib.load()
+    lib = _lib.load(_lib.DEBUG_LIB_PATH)
     lib.mavg_test_ahead_schedule(sched.get("slots", -1), sched.get("spin", -1))
     try:
-        return fn()
+        return fn(_lib.DEBUG_LIB_PATH)
     finally:
         lib.mavg_test_ahead_schedule(-1, -1)
 
@@ -499,8 +505,8 @@ def test_ahead_records_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, 
     else:
         x = oracle_mod.synth_i16(frames * C, seed=77)
     base = _run(x, k, C, "auto", gpu)
-    for sched in ({"spin": 0}, {"slots": 0}, {"slots": 8}, {"slots": 1 << 28}, {"slots": 8, "spin": 0}):
-        y = _with_schedule(sched, lambda: _run(x, k, C, "auto", gpu))
+    for sched in ({}, {"spin": 0}, {"slots": 0}, {"slots": 8}, {"slots": 1 << 28}, {"slots": 8, "spin": 0}):
+        y = _with_schedule(sched, lambda lib: _run(x, k, C, "auto", gpu, library=lib))
         assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), sched
     if dtype == "f32":
         r = oracle_mod.check_synth_exact(base, k, C, seed=77, dist=2, rtol=RTOL)
@@ -528,7 +534,8 @@ def test_hillis_long_windows_through_the_record_carry(oracle_mod, gpu, C, k, dt)
         else:
             x = dsp.fill_synthetic(frames * C, torch.int16, seed=31, device=gpu)
         y = dsp.moving_average(x, k, channels=C, algo=algo).cpu().numpy()
-        y0 = _with_schedule({"spin": 0, "slots": 0}, lambda: dsp.moving_average(x, k, channels=C, algo=algo).cpu().numpy())
+        y0 = _with_schedule({"spin": 0, "slots": 0},
+                            lambda lib: dsp.moving_average(x, k, channels=C, algo=algo, library=lib).cpu().numpy())
         assert np.array_equal(y.view(np.uint8), y0.view(np.uint8)), algo
         r = oracle_mod.check_synth(y, k, C, seed=31, dist=2 if dt == "f32" else 0, rtol=RTOL)
         assert r["mismatches"] == 0, (algo, r)
@@ -549,8 +556,8 @@ def test_self_published_records(oracle_mod, gpu, k):
     assert "self=1" not in dsp.plan(frames, k, 1, dsp.F32, "hillis")
     x = oracle_mod.synth_f32(frames, seed=91, dist=2)
     base = _run(x, k, 1, "auto", gpu)
-    for sched in ({"spin": 0}, {"slots": 0}, {"slots": 8, "spin": 0}):
-        y = _with_schedule(sched, lambda: _run(x, k, 1, "auto", gpu))
+    for sched in ({}, {"spin": 0}, {"slots": 0}, {"slots": 8, "spin": 0}):
+        y = _with_schedule(sched, lambda lib: _run(x, k, 1, "auto", gpu, library=lib))
         assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), sched
     r = oracle_mod.check_synth_exact(base, k, 1, seed=91, dist=2, rtol=RTOL)
     assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, r
@@ -583,6 +590,12 @@ def test_f32_four_channels_in_wide_units(oracle_mod, gpu, C, k):
     yb = torch.zeros_like(xb)
     dsp.moving_average_into(xb[4:], yb[4:], k, C, "blelloch")
     assert_f32_close(yb[4:].cpu().numpy(), ref, f"k={k} 16-B view")
+    if C == 8:  # a whole frame in: 32-B aligned views, not 64-B aligned (the wide units' loads and stores)
+        xb = torch.zeros(frames * C + 8, dtype=torch.float32, device=gpu)
+        xb[8:] = torch.from_numpy(x).to(gpu)
+        yb = torch.zeros_like(xb)
+        dsp.moving_average_into(xb[8:], yb[8:], k, C, "blelloch")
+        assert_f32_close(yb[8:].cpu().numpy(), ref, f"k={k} 32-B view")
     assert_f32_close(_run(x, k, C, "blelloch_scalar", gpu), ref, f"k={k} scalar")
 
 

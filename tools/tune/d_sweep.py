@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Look-ahead distance sweep in bench.py's environment: the library's own
 dispatch with D (dispatch slots between a tile and the tile whose record it
-publishes) forced through the test hook mavg_test_ahead_schedule, interleaved
-rounds, one HIP-event pair per launch on torch's current stream.  D also sets
-the window-matched run length for windows past the L2 reach (ahead_run_length).
+publishes) forced through the test hook mavg_test_ahead_schedule (include/mavg_debug.h),
+interleaved rounds, one HIP-event pair per launch on torch's current stream.
+The hook exists only in builds with MAVG_TEST_HOOKS: this tool loads the
+release-flag build with the hooks (`make -C digital_signal_processsing_amd/csrc hooks`
+-> lib/libmavg_hooks.so; no device checks, so the timing is the release code's).
+The forced D changes only the producer distance; the window-matched run length
+stays the tuned schedule's (ahead_run_length of the default D).
 
     python tools/tune/d_sweep.py --k 4000000 --c 1 --dtype f32 --slots 256 512 768 1024
 """
@@ -33,7 +37,8 @@ def main():
     n = 1 << a.log2n
     tdt = torch.int16 if a.dtype == "i16" else torch.float32
     code = dsp.I16 if a.dtype == "i16" else dsp.F32
-    lib = _lib.load()
+    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libmavg_hooks.so")
+    lib = _lib.load(path)
     x = dsp.fill_synthetic(n, tdt, seed=0x5EED, device="cuda")
     y = torch.empty_like(x)
     ref = None
@@ -43,12 +48,12 @@ def main():
         for d in (a.slots if rnd % 2 == 0 else a.slots[::-1]):
             lib.mavg_test_ahead_schedule(d, -1)
             try:
-                plans[d] = dsp.plan(n, a.k, a.c, code)
-                dsp.moving_average_into(x, y, a.k, a.c)  # warm-up (and the workspace)
+                plans[d] = dsp.plan(n, a.k, a.c, code, library=path)
+                dsp.moving_average_into(x, y, a.k, a.c, library=path)  # warm-up (and the workspace)
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
                 for e0, e1 in ev:
                     e0.record()
-                    dsp.moving_average_into(x, y, a.k, a.c)
+                    dsp.moving_average_into(x, y, a.k, a.c, library=path)
                     e1.record()
                 torch.cuda.synchronize()
                 times[d] += [e0.elapsed_time(e1) for e0, e1 in ev]
