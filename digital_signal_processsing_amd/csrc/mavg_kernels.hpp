@@ -12,6 +12,9 @@
 //   mavg_tile.hpp      tile_scan_kernel: one short-lived workgroup per flat
 //                      tile; the carry is rebuilt from a k-frame halo staged
 //                      in LDS.  The default for windows up to ~16 KiB of halo.
+//   mavg_wide.hpp      wide_tile_kernel: the tile scan for multi-channel
+//                      frames, lanes own 64/128-B chunks of consecutive
+//                      frames read from a swizzled LDS stage.
 //   mavg_lookback.hpp  ahead_scan_kernel: one pass over HBM, carry from
 //                      whole-tile records that tiles D slots ahead published
 //                      inside the launch; windows past the LDS-staged halo,
@@ -35,3 +38,4 @@
 #include "mavg_lookback.hpp"
 #include "mavg_misc.hpp"
 #include "mavg_tile.hpp"
+#include "mavg_wide.hpp"

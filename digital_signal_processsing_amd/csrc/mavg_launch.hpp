@@ -147,6 +147,49 @@ int launch_tile_scan(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
+// wide-frame tile scan (mavg_wide.hpp): lanes own chunks of P consecutive
+// frames (64 or 128 B) of a multi-channel signal; 16-B-aligned views only
+// (the host's vector path), halo + tile staged in a swizzled LDS stage.
+template <typename T, typename A, int C, int P, int U, int WG, int NT, int DV = 0>
+int launch_wide_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
+  constexpr int EPG = 16 / (int)sizeof(T);
+  constexpr int G = P * C / EPG;
+  constexpr int TF = WG * P * U;
+  constexpr int TG = WG * U * G;
+  constexpr int NSEG = U * (WG / 64);
+  const long long nframes = sg.nframes;
+  const long long hg = ((long long)k * C + EPG - 1) / EPG;  // granules covering the k-frame halo
+  const long long Hg = (hg + 15) / 16 * 16;                // whole 256-B LDS rows
+  const size_t lds = (size_t)(Hg + TG) * 16 + (size_t)(NSEG + WG / 64) * C * sizeof(A);
+  if (lds > 80 * 1024) return MAVG_ERR_UNSUPPORTED;  // two workgroups per CU at the longest halos
+  const long long ntiles = (nframes + TF - 1) / TF;
+  if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text),
+             "wide_tile<%s,acc=%s,C=%d,P=%d,U=%d,nt=%d,dv=%d> grid=%lld block=%d lds=%zu tile_frames=%d remap=%d",
+             type_name<T>(), type_name<A>(), C, P, U, NT, DV, ntiles, WG, lds, TF, xcd_remap);
+    return MAVG_OK;
+  }
+  WideParams p{};
+  p.in = sg.in;
+  p.out = sg.out;
+  p.hist = sg.hist;
+  p.nframes = nframes;
+  p.ntiles = ntiles;
+  p.k = k;
+  p.halo_g = (int)Hg;
+  p.xk_off = (int)((EPG - ((long long)k * C) % EPG) % EPG);
+  p.xcd_remap = xcd_remap;
+  p.pre = sg.pre;
+  p.o = make_out_params(k);
+  if (lds > 64 * 1024) {
+    const int s = raise_dyn_lds_limit<&wide_tile_kernel<T, A, C, P, U, WG, NT, DV>>(80 * 1024);
+    if (s != MAVG_OK) return s;
+  }
+  hipLaunchKernelGGL((wide_tile_kernel<T, A, C, P, U, WG, NT, DV>), dim3((unsigned)ntiles), dim3(WG), lds, st, p);
+  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+}
+
 // look-ahead scan (one pass over HBM): zero the record granules, then one
 // launch whose tile t publishes the records of tile t + ahead and scans
 // tile t with its carry from earlier records (mavg_lookback.hpp).
@@ -479,9 +522,45 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
   }
 }
 
+// The wide-frame tile scan (mavg_wide.hpp) for multi-channel fp32 frames
+// while its halo fits the LDS stage; MAVG_ERR_UNSUPPORTED otherwise (the
+// caller falls back to the unit kernels).  Shapes from the in-process A/B
+// against the round-3 unit kernels (tools/tune/wide_ab.hip, 2^30 samples,
+// fraction of 8 TB/s, profiles/r04_tuning/wide/):
+//   C=2  k=7 0.693 -> 0.790 (P8 U1), k=1024 0.645 -> 0.784, k=2048 0.649 ->
+//        0.781, k=4096 0.662 (look-ahead) -> 0.700 (P16 U1: 4096-frame tiles)
+//   C=4  k=7 0.651 -> 0.776, k=256 0.650 -> 0.794 (P8 U2), k=1024 0.506 ->
+//        0.774, k=2048 0.509 (look-ahead) -> 0.665 (P8 U1)
+//   C=8  k=7 0.416 -> 0.794 (P4 x 128 threads), k=256 0.259 -> 0.700, k=512
+//        0.237 -> 0.671, k=1024 0.234 -> 0.537 (P4 U1; 64 KiB of stage, two
+//        workgroups per CU)
+template <typename T, typename A, int C>
+int dispatch_wide(const Sig& sg, int k, hipStream_t st) {
+  constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
+  const long long halo_bytes = (long long)k * C * (long long)sizeof(T);
+  if constexpr (sizeof(T) == 4 && C == 2) {
+    if (halo_bytes <= 2048) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
+    if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 16, 1, kWG, kNtS>(sg, k, st);
+  } else if constexpr (sizeof(T) == 4 && C == 4) {
+    if (halo_bytes <= 4096) return launch_wide_tile<T, A, C, 8, 2, kWG, kNtS>(sg, k, st);
+    if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
+  } else if constexpr (sizeof(T) == 4 && C == 8) {
+    if (halo_bytes <= 256) return launch_wide_tile<T, A, C, 4, 1, 128, kNtS>(sg, k, st);
+    if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 4, 1, kWG, kNtS>(sg, k, st);
+  }
+  (void)halo_bytes;
+  return MAVG_ERR_UNSUPPORTED;
+}
+
 template <typename T, typename A, int C>
 int dispatch_scan_c(bool vec, bool hs, const Sig& sg, int k, int block, hipStream_t st, Workspace ws) {
   constexpr int VF = (C * (int)sizeof(T) <= 16 && 16 % (C * (int)sizeof(T)) == 0) ? 16 / (C * (int)sizeof(T)) : 0;
+  if constexpr (sizeof(T) == 4 && (C == 2 || C == 4 || C == 8)) {
+    if (vec && !hs && !sg.eio && block == 0) {
+      const int s = dispatch_wide<T, A, C>(sg, k, st);
+      if (s != MAVG_ERR_UNSUPPORTED) return s;
+    }
+  }
   // fp32 with 8 channels (32-B frames, no vector form): past the 1-frame
   // tiles' LDS-staged halo (8 KiB, k > 256) the look-ahead scan takes 2 frames
   // per lane as well; below it the 1-frame tiles stay (the 64-B-unit tile

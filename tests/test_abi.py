@@ -123,8 +123,13 @@ def test_plan_describes_launch_without_gpu():
     # split cache policy (nt tile loads but the halo tail, nt halo, nt stores)
     assert "nt=13" in p and "nt=13" in dsp.plan(1 << 30, 4096) and "nt=13" in dsp.plan(1 << 30, 64), p
     assert "U=4" in dsp.plan(1 << 30, 4096) and "block=512" in dsp.plan(1 << 30, 4096)
-    # stereo fp32 keeps the register-staged tile
-    assert "dma=0" in dsp.plan(1 << 30, 1024, channels=2)
+    # multi-channel fp32 frames: the wide-frame tile (chunks of consecutive frames per lane)
+    assert dsp.plan(1 << 30, 1024, channels=2).startswith("wide_tile<f32,acc=f64,C=2,P=16,U=1")
+    assert dsp.plan(1 << 30, 1024, channels=4).startswith("wide_tile<f32,acc=f64,C=4,P=8,U=1")
+    assert dsp.plan(1 << 30, 1024, channels=8).startswith("wide_tile<f32,acc=f64,C=8,P=4,U=1")
+    assert dsp.plan(1 << 30, 1025, channels=8).startswith("ahead_scan<f32,acc=f64,C=8,F=2")
+    assert dsp.plan(3 << 28, 1024, channels=3).startswith("tile_scan<f32")  # 12-B frames: frame units
+    assert dsp.plan(1 << 30, 1024, channels=2, algo="hillis").startswith("tile_scan<")
     # int16 keeps the register-staged tiles (bench.py's timing, tools/tune/ab_libs.py)
     i16 = lambda k, c=1: dsp.plan(1 << 30, k, channels=c, dtype=dsp.I16)
     for k, c in ((1024, 1), (1023, 1), (1024, 2), (512, 2)):

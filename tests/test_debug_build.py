@@ -90,11 +90,13 @@ assert "self=1" in dsp.plan(3_000_017, 8192, 1, dsp.F32)
 xf = oracle.synth_f32(3_000_017, seed=7, dist=2)
 r = oracle.check_synth_exact(run(xf, 8192, 1, "auto"), 8192, 1, seed=7, dist=2)
 assert r["mismatches"] == 0, r
-# 8 fp32 channels: the look-ahead scan's 64-B units (2 frames per lane)
-assert ",C=8,F=2," in dsp.plan(300_007 * 8, 1024, 8, dsp.F32)
-xf = oracle.synth_f32(300_007 * 8, seed=8, dist=1)
-y, rf = run(xf, 1024, 8, "auto").astype(np.float64), oracle.mavg_f32(xf, 1024, 8).astype(np.float64)
-assert (np.abs(y - rf) <= 1e-5 * np.maximum(np.abs(rf), 1e-30)).all()
+# 8 fp32 channels: the wide tile (k <= 1024) and the look-ahead scan's 64-B units past it;
+# stereo fp32 with an odd window (the half-granule x[n-k] extraction)
+for C, k, kern in ((8, 1024, "wide_tile<"), (8, 3000, "ahead_scan<"), (2, 1023, "wide_tile<"), (4, 7, "wide_tile<")):
+    assert dsp.plan(300_007 * C, k, C, dsp.F32).startswith(kern), (C, k)
+    xf = oracle.synth_f32(300_007 * C, seed=8, dist=1)
+    y, rf = run(xf, k, C, "auto").astype(np.float64), oracle.mavg_f32(xf, k, C).astype(np.float64)
+    assert (np.abs(y - rf) <= 1e-5 * np.maximum(np.abs(rf), 1e-30)).all(), (C, k)
 torch.cuda.synchronize()
 print("debug build ok")
 '''

@@ -568,34 +568,95 @@ def test_self_published_records(oracle_mod, gpu, k):
     assert_f32_close(_run(xf[cut:], k, 1, "blelloch", gpu, history=hist), full[cut:], f"k={k} history")
 
 
-@pytest.mark.parametrize("C,k", [(4, 1), (4, 7), (4, 64), (4, 256), (4, 257), (4, 500), (4, 1001), (4, 2000),
-                                 (4, 44_100), (8, 7), (8, 256), (8, 257), (8, 1024), (8, 44_100)])
-def test_f32_four_channels_in_wide_units(oracle_mod, gpu, C, k):
-    """fp32 with 4 channels runs the Blelloch flavour in 32-B units (two
-    frames per lane): the tile scan up to 4 KiB of halo, the look-ahead scan
-    past it, also for windows shorter than its 1024-frame tile; with 8
-    channels the look-ahead scan (k > 256) takes 64-B units.  Rounding data
-    against the oracle, a view 16 B into an allocation (16-B but not 32-B
-    aligned), and the frame-unit form (blelloch_scalar) for comparison."""
+def _wide_windows(dsp, C):
+    """Windows around every shape change of the wide tile (halo rows, tile
+    length, the last window it takes) and a few inside each range."""
+    n = 1 << 24
+    ks = {1, 2, 3, 7, 8, 9, 63, 64, 65}
+    for k in range(1, 9000):
+        if dsp.plan(n, k, C, dsp.F32) != dsp.plan(n, k + 1, C, dsp.F32):
+            ks.update({k - 1, k, k + 1, k + 2})
+    tf = int(dsp.plan(n, 1, C, dsp.F32).split("tile_frames=")[1].split()[0])
+    ks.update({tf - 1, tf, tf + 1})
+    return sorted(k for k in ks if k >= 1)
+
+
+@pytest.mark.parametrize("C", [2, 4, 8])
+def test_wide_tile_every_window_edge(oracle_mod, gpu, C):
+    """fp32 multi-channel frames run the wide-frame tile scan (mavg_wide.hpp:
+    chunks of P consecutive frames per lane, swizzled LDS stage, outputs through
+    LDS): every window where the plan changes (halo rows, tile shapes, the switch
+    to the look-ahead scan) and one frame either side, odd windows (the
+    half-granule x[n-k] shift at C=2), on rounding data (dist 2) against the
+    exact window sums, with a ragged tail tile."""
+    import digital_signal_processsing_amd as dsp
+    frames = 3 * 4096 + 1237
+    seen = set()
+    for k in _wide_windows(dsp, C):
+        plan = dsp.plan(frames * C, k, C, dsp.F32)
+        seen.add(plan.split(" grid")[0])
+        x = oracle_mod.synth_f32(frames * C, seed=k, dist=2)
+        r = oracle_mod.check_synth_exact(_run(x, k, C, "blelloch", gpu), k, C, seed=k, dist=2, rtol=RTOL)
+        assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, (k, plan, r)
+    assert any(p.startswith("wide_tile<") for p in seen) and any(p.startswith("ahead_scan<") for p in seen), seen
+
+
+@pytest.mark.parametrize("C,k", [(2, 1), (2, 7), (2, 1023), (2, 1024), (2, 4096), (4, 1), (4, 255), (4, 1024),
+                                 (4, 2048), (8, 1), (8, 8), (8, 9), (8, 1000), (8, 1024)])
+def test_wide_tile_short_signals_history_and_views(oracle_mod, gpu, C, k):
+    """The wide tile's edge paths: signals shorter than a tile and than the
+    window (every tile an edge tile), a history (the window reaching before
+    frame 0, element-staged first tiles), views 16 B into an allocation (C=2: a
+    peeled 2-frame head then the body with pre=2; C=4: 16-B aligned frames; C=8:
+    32-B-aligned views), against the oracle."""
+    import digital_signal_processsing_amd as dsp
+    import torch
+    assert dsp.plan(1 << 24, k, C, dsp.F32).startswith("wide_tile<"), dsp.plan(1 << 24, k, C, dsp.F32)
+    for frames in (1, 5, k, 2 * k + 3, 100_003):
+        x = oracle_mod.synth_f32(frames * C, offset=frames + k, dist=1)
+        assert_f32_close(_run(x, k, C, "blelloch", gpu), oracle_mod.mavg_f32(x, k, C), f"frames={frames}")
+    frames = 100_003
+    x = oracle_mod.synth_f32(frames * C, offset=3, dist=1)
+    full = oracle_mod.mavg_f32(x, k, C)
+    cut = 3 * k + 11
+    lo = max(0, cut - (k - 1))
+    hist = np.zeros((k - 1) * C, dtype=np.float32)
+    hist[(k - 1 - (cut - lo)) * C:] = x[lo * C: cut * C]
+    assert_f32_close(_run(x[cut * C:], k, C, "blelloch", gpu, history=hist), full[cut * C:], "history")
+    off = 8 if C == 8 else 4  # 32 B (C=8) or 16 B
+    xb = torch.zeros(frames * C + off, dtype=torch.float32, device=gpu)
+    xb[off:] = torch.from_numpy(x).to(gpu)
+    yb = torch.zeros_like(xb)
+    dsp.moving_average_into(xb[off:], yb[off:], k, C, "blelloch")
+    assert_f32_close(yb[off:].cpu().numpy(), full, f"view +{off * 4} B")
+    if C == 2:  # 8 B in: a one-frame head, then the 16-B aligned body (pre=1)
+        xb = torch.zeros(frames * C + 2, dtype=torch.float32, device=gpu)
+        xb[2:] = torch.from_numpy(x).to(gpu)
+        yb = torch.zeros_like(xb)
+        dsp.moving_average_into(xb[2:], yb[2:], k, C, "blelloch")
+        assert_f32_close(yb[2:].cpu().numpy(), full, "view +8 B")
+
+
+@pytest.mark.parametrize("C,k", [(4, 4097), (4, 44_100), (8, 1025), (8, 44_100), (2, 4097)])
+def test_f32_wide_units_past_the_wide_tile(oracle_mod, gpu, C, k):
+    """Past the wide tile's LDS-staged halo the look-ahead scan runs in 32-B
+    (C=4) or 64-B (C=8) units: rounding data against the exact sums, a view 16
+    B (C=8: 32 B) into an allocation, and the frame-unit form for comparison."""
     import digital_signal_processsing_amd as dsp
     import torch
     frames = 300_007
     plan = dsp.plan(frames * C, k, C, dsp.F32)
-    assert (f",C={C},F=2," in plan) == (C == 4 or k > 256), plan
-    x = oracle_mod.synth_f32(frames * C, offset=k, dist=1)
+    assert plan.startswith("ahead_scan<") and ((f",C={C},F=2," in plan) == (C != 2)), plan
+    x = oracle_mod.synth_f32(frames * C, seed=k, dist=2)
+    r = oracle_mod.check_synth_exact(_run(x, k, C, "blelloch", gpu), k, C, seed=k, dist=2, rtol=RTOL)
+    assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, (plan, r)
     ref = oracle_mod.mavg_f32(x, k, C)
-    assert_f32_close(_run(x, k, C, "blelloch", gpu), ref, f"k={k}")
-    xb = torch.zeros(frames * C + 4, dtype=torch.float32, device=gpu)
-    xb[4:] = torch.from_numpy(x).to(gpu)
+    off = 8 if C == 8 else 4
+    xb = torch.zeros(frames * C + off, dtype=torch.float32, device=gpu)
+    xb[off:] = torch.from_numpy(x).to(gpu)
     yb = torch.zeros_like(xb)
-    dsp.moving_average_into(xb[4:], yb[4:], k, C, "blelloch")
-    assert_f32_close(yb[4:].cpu().numpy(), ref, f"k={k} 16-B view")
-    if C == 8:  # a whole frame in: 32-B aligned views, not 64-B aligned (the wide units' loads and stores)
-        xb = torch.zeros(frames * C + 8, dtype=torch.float32, device=gpu)
-        xb[8:] = torch.from_numpy(x).to(gpu)
-        yb = torch.zeros_like(xb)
-        dsp.moving_average_into(xb[8:], yb[8:], k, C, "blelloch")
-        assert_f32_close(yb[8:].cpu().numpy(), ref, f"k={k} 32-B view")
+    dsp.moving_average_into(xb[off:], yb[off:], k, C, "blelloch")
+    assert_f32_close(yb[off:].cpu().numpy(), ref, f"k={k} view")
     assert_f32_close(_run(x, k, C, "blelloch_scalar", gpu), ref, f"k={k} scalar")
 
 

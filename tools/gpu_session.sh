@@ -29,6 +29,8 @@ for step in "$@"; do
     test) run pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=30 -p no:cacheprovider ;;
     testx) run pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread \
             -p no:cacheprovider ;;
+    testm) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v --maxfail=10 --timeout 200 --timeout-method thread \
+            -p no:cacheprovider ;;
     bench) run bench 400 python bench.py --steps 20 --warmup 5 --all-workloads ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
             python bench.py --steps 10 --warmup 3 --no-cpu-baseline --all-workloads ;;
@@ -43,7 +45,6 @@ for step in "$@"; do
             --master-port 29512 bench.py --gpus 4 --steps 3 --warmup 1 --dist-backend gloo --check ;;
     dist2) run pytest_dist2 600 python -u -m pytest tests/test_gpu_fullsize.py -m gpu -k rounding -s -q \
             --timeout 170 --timeout-method thread -p no:cacheprovider ;;
-    dab) run direct_ab 200 bash tools/gpu/r03_direct_ab.sh "$TAG" ;;
     full) run pytest_full 900 python -u -m pytest tests/test_gpu_fullsize.py tests/test_bench_launch.py -m gpu -x -v \
             --timeout 170 --timeout-method thread -p no:cacheprovider ;;
     # the driver's exact bench command, then the same command under the kernel tracer

@@ -1,0 +1,179 @@
+// wide_ab.hip -- in-process A/B of the wide-frame tile scan (mavg_wide.hpp)
+// shapes against the library's own dispatch for multi-channel fp32 signals,
+// interleaved rounds, one HIP-event pair per launch (bench.py's timing), the
+// library's flat copy as the same-box ceiling.  Every variant's output is
+// checked against the library's (|dy| <= 1e-6 |y|, fp64 sums in another order).
+//
+// build: make -C tools/tune wide_ab
+// run:   tools/tune/wide_ab <log2n> <k> <C> [rounds] [dist]
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../digital_signal_processsing_amd/csrc/mavg_launch.hpp"
+
+using namespace mavg;
+
+#define CK(x)                                                                                 \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) {                                                                   \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      exit(1);                                                                                \
+    }                                                                                         \
+  } while (0)
+
+struct Var {
+  std::string name;
+  std::function<int(hipStream_t)> run;
+  std::vector<float> ms;
+};
+
+template <int C, int P, int U, int WG = 256>
+void add1(std::vector<Var>& vs, const Sig& sg, int k) {
+  constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
+  char name[64];
+  snprintf(name, sizeof name, "wide P%d U%d %d ntS", P, U, WG);
+  vs.push_back({name, [=](hipStream_t s) { return launch_wide_tile<float, double, C, P, U, WG, kNtS>(sg, k, s); }, {}});
+}
+
+// the round-3 unit kernels for the same C (tile_scan / ahead_scan, 32-B or 64-B units)
+template <int C, int F>
+void add_unit(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
+  char name[64];
+  snprintf(name, sizeof name, "r03 units F=%d", F);
+  vs.push_back({name, [=](hipStream_t s) { return dispatch_scan_f<float, double, C, F, false>(sg, k, 0, s, ws); }, {}});
+}
+
+template <int C>
+void add_wide(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
+  if constexpr (C == 2) {
+    add_unit<C, 2>(vs, sg, k, ws);
+    add1<C, 8, 1>(vs, sg, k);
+    add1<C, 8, 2>(vs, sg, k);
+    add1<C, 16, 1>(vs, sg, k);
+    add1<C, 16, 1, 128>(vs, sg, k);
+  } else if constexpr (C == 4) {
+    add_unit<C, 2>(vs, sg, k, ws);
+    add1<C, 4, 2>(vs, sg, k);
+    add1<C, 8, 1>(vs, sg, k);
+    add1<C, 8, 2>(vs, sg, k);
+    add1<C, 8, 1, 128>(vs, sg, k);
+  } else {
+    add_unit<C, 2>(vs, sg, k, ws);
+    add_unit<C, 1>(vs, sg, k, ws);
+    add1<C, 4, 1>(vs, sg, k);
+    add1<C, 4, 1, 128>(vs, sg, k);
+    add1<C, 4, 2, 128>(vs, sg, k);
+  }
+}
+
+int main(int argc, char** argv) {
+  const int lg = argc > 1 ? atoi(argv[1]) : 30;
+  const int k = argc > 2 ? atoi(argv[2]) : 1024;
+  const int C = argc > 3 ? atoi(argv[3]) : 4;
+  const int rounds = argc > 4 ? atoi(argv[4]) : 6;
+  const int dist = argc > 5 ? atoi(argv[5]) : 1;
+  const int steps = 10;
+  const long long n = 1LL << lg;
+  float *x, *y, *yref;
+  CK(hipMalloc(&x, n * 4));
+  CK(hipMalloc(&y, n * 4));
+  CK(hipMalloc(&yref, n * 4));
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  if (mavg_fill_synthetic(x, n, MAVG_F32, 0x5EED, 0, dist, st) != MAVG_OK) return 1;
+  size_t wsb = 0;
+  mavg_workspace_bytes(n, C, k, MAVG_F32, MAVG_ALGO_BLELLOCH, 0, &wsb);
+  const size_t ws2 = std::max<size_t>(wsb, 256u << 20);  // also the r03 unit kernels' look-ahead records
+  void* ws = nullptr;
+  CK(hipMalloc(&ws, ws2));
+  char plan[256];
+  mavg_plan(n, C, k, MAVG_F32, MAVG_ALGO_BLELLOCH, 0, plan, sizeof plan);
+
+  Sig sg{x, y, nullptr, n / C};
+  std::vector<Var> vs;
+  vs.push_back({std::string("lib: ") + plan, [=](hipStream_t s) {
+                  return mavg_run(x, y, n, C, k, MAVG_F32, MAVG_ALGO_BLELLOCH, 0, nullptr, ws, wsb, s);
+                }, {}});
+  vs.push_back({"copy", [=](hipStream_t s) { return mavg_stream_copy(x, y, n * 4, s); }, {}});
+  switch (C) {
+    case 2: add_wide<2>(vs, sg, k, Workspace{ws, ws2}); break;
+    case 4: add_wide<4>(vs, sg, k, Workspace{ws, ws2}); break;
+    case 8: add_wide<8>(vs, sg, k, Workspace{ws, ws2}); break;
+    default: fprintf(stderr, "C must be 2, 4 or 8\n"); return 1;
+  }
+  // reference output: the library
+  if (vs[0].run(st) != MAVG_OK) return 1;
+  CK(hipMemcpyAsync(yref, y, n * 4, hipMemcpyDeviceToDevice, st));
+  CK(hipStreamSynchronize(st));
+  std::vector<float> href(n), h(n);
+  CK(hipMemcpy(href.data(), yref, n * 4, hipMemcpyDeviceToHost));
+  for (size_t v = 2; v < vs.size(); ++v) {
+    CK(hipMemsetAsync(y, 0xff, n * 4, st));
+    const int rc = vs[v].run(st);
+    CK(hipStreamSynchronize(st));
+    if (rc != MAVG_OK) {
+      printf("%-40s rc=%d (skipped)\n", vs[v].name.c_str(), rc);
+      vs[v].run = nullptr;
+      continue;
+    }
+    CK(hipMemcpy(h.data(), y, n * 4, hipMemcpyDeviceToHost));
+    long long bad = 0;
+    double worst = 0;
+    for (long long i = 0; i < n; ++i) {
+      const double r = href[i], d = std::fabs((double)h[i] - r);
+      const double rel = d / std::max(std::fabs(r), 1e-30);
+      if (!(d <= 1e-6 * std::fabs(r) || d == 0.0)) {
+        if (bad < 5) printf("  mismatch %s at %lld: %.9g vs %.9g\n", vs[v].name.c_str(), i, h[i], r);
+        ++bad;
+      }
+      if (d != 0.0 && rel > worst) worst = rel;
+    }
+    g_plan = nullptr;
+    printf("%-40s check: %lld bad, max rel %.3g\n", vs[v].name.c_str(), bad, worst);
+    if (bad) vs[v].run = nullptr;
+  }
+  hipEvent_t e0[steps], e1[steps];
+  for (int i = 0; i < steps; ++i) {
+    CK(hipEventCreate(&e0[i]));
+    CK(hipEventCreate(&e1[i]));
+  }
+  for (int r = 0; r < rounds; ++r) {
+    for (size_t vi = 0; vi < vs.size(); ++vi) {
+      Var& v = vs[(r & 1) ? vs.size() - 1 - vi : vi];
+      if (!v.run) continue;
+      v.run(st);  // warm
+      for (int i = 0; i < steps; ++i) {
+        CK(hipEventRecord(e0[i], st));
+        v.run(st);
+        CK(hipEventRecord(e1[i], st));
+      }
+      CK(hipStreamSynchronize(st));
+      for (int i = 0; i < steps; ++i) {
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0[i], e1[i]));
+        v.ms.push_back(ms);
+      }
+    }
+  }
+  printf("n=2^%d k=%d C=%d rounds=%d dist=%d (fraction of 8 TB/s, mean of per-launch events)\n", lg, k, C, rounds,
+         dist);
+  for (auto& v : vs) {
+    if (v.ms.empty()) continue;
+    double m = 0;
+    for (float t : v.ms) m += t;
+    m /= v.ms.size();
+    std::vector<float> s = v.ms;
+    std::sort(s.begin(), s.end());
+    const double md = s[s.size() / 2];
+    printf("%-72s mean %.4f ms  %.4f   median %.4f\n", v.name.c_str(), m, 8.0 * n / (m * 1e-3) / 8e12, 8.0 * n / (md * 1e-3) / 8e12);
+  }
+  return 0;
+}
