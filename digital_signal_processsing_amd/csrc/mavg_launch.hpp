@@ -50,7 +50,7 @@ int raise_dyn_lds_limit(int bytes) {
 // Dry-run support for mavg_plan(): when g_plan is set (thread-local), the
 // launchers describe the launch they would make instead of making it.
 struct LaunchPlan {
-  char text[160];
+  char text[256];  // the longest plan (look-ahead with runs) is ~170 characters
   size_t ws_bytes;  // device workspace the launch needs (mavg_workspace_bytes)
 };
 extern thread_local LaunchPlan* g_plan;
@@ -399,6 +399,79 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   return s;
 }
 
+// wide look-ahead scan (mavg_wide.hpp): the look-ahead record carry in its
+// unit layout (F frames x U units per lane, per-tile records) with the wide
+// in-tile scan (P-frame chunks x UW rows); 16-B-aligned views only.
+template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U>
+int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
+  constexpr int NW = WG / 64;
+  constexpr int EPG = 16 / (int)sizeof(T);
+  constexpr int G = P * C / EPG;
+  constexpr int TF = WG * P * UW;
+  constexpr int TG = WG * UW * G;
+  constexpr int NSEG = UW * NW;
+  using SA = typename ScanAcc<T, A>::type;
+  const long long nframes = sg.nframes;
+  ahead &= ~7;
+  const int ahead_plan = ahead;
+  int spin = kAheadSpin;
+#ifdef MAVG_TEST_HOOKS
+  {
+    const int t = g_test_ahead_slots.load(std::memory_order_relaxed);
+    if (t >= 0) ahead = t & ~7;
+  }
+  {
+    const int t = g_test_ahead_spin.load(std::memory_order_relaxed);
+    if (t >= 0) spin = t;
+  }
+#endif
+  const int xcd_remap = ahead_past_l2(k, C, sizeof(T), TF) ? ahead_run_length(k, TF, ahead_plan) : 1;
+  const long long ntiles = (nframes + TF - 1) / TF;
+  const long long nfull = nframes / TF;
+  if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  const size_t need = ahead_granule_bytes<T, A, C, F, U>(nfull);  // per-tile records + 16
+  const size_t lds = (size_t)(2 * TG + 1) * 16 + (size_t)NW * C * sizeof(A) + (size_t)(NSEG + 3 * NW) * C * sizeof(SA);
+  if (lds > 80 * 1024) return MAVG_ERR_UNSUPPORTED;
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text),
+             "wide_ahead<%s,acc=%s,C=%d,P=%d,U=%d,nt=%d,dv=%d,F=%d,FU=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
+             "ahead=%d remap=%d ws=%zu",
+             type_name<T>(), type_name<A>(), C, P, UW, NT, DV, F, U, ntiles, WG, lds, TF, ahead, xcd_remap, need);
+    g_plan->ws_bytes = need;
+    return MAVG_OK;
+  }
+  if (ws.ptr == nullptr || ws.bytes < need) return MAVG_ERR_WORKSPACE;
+  if ((reinterpret_cast<uintptr_t>(ws.ptr) & 15u) != 0) return MAVG_ERR_MISALIGNED;
+  if (hipMemsetAsync(ws.ptr, 0, need, st) != hipSuccess) return MAVG_ERR_HIP;
+  AheadParams p{};
+  p.in = sg.in;
+  p.out = sg.out;
+  p.hist = sg.hist;
+  p.nframes = nframes;
+  p.pre = sg.pre;
+  p.eio = 0;
+  p.nfull = nfull;
+  p.k = k;
+  p.o = make_out_params(k);
+  p.halo_units = (k + F - 1) / F;
+  p.xk_off = (((F - k % F) % F) * C) % EPG;
+  p.xcd_remap = xcd_remap;
+  p.runs_done = 0;
+  p.ahead = ahead;
+  p.head = xcd_remap == 1 ? (int)std::min<long long>((long long)k / TF, nfull) : 0;
+  p.spin = spin;
+  p.self = 0;
+  p.gran = static_cast<unsigned long long*>(ws.ptr);
+  p.runs = nullptr;
+  p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
+  if (lds > 64 * 1024) {
+    const int s = raise_dyn_lds_limit<&wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U>>(80 * 1024);
+    if (s != MAVG_OK) return s;
+  }
+  hipLaunchKernelGGL((wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U>), dim3((unsigned)ntiles), dim3(WG), lds, st, p);
+  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+}
+
 // Algorithm selection for the scan family (measured on MI355X with
 // tools/tune/tune_scan.hip + tools/tune/sweep_*.sh, 2^30 samples, back-to-back
 // launches; DESIGN.md "Tuning").  Tiles are 4 KiB of samples per U.
@@ -535,7 +608,7 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
 //        0.237 -> 0.671, k=1024 0.234 -> 0.537 (P4 U1; 64 KiB of stage, two
 //        workgroups per CU)
 template <typename T, typename A, int C>
-int dispatch_wide(const Sig& sg, int k, hipStream_t st) {
+int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
   const long long halo_bytes = (long long)k * C * (long long)sizeof(T);
   if constexpr (sizeof(T) == 4 && C == 2) {
@@ -548,7 +621,14 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st) {
     if (halo_bytes <= 256) return launch_wide_tile<T, A, C, 4, 1, 128, kNtS>(sg, k, st);
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 4, 1, kWG, kNtS>(sg, k, st);
   }
+  // past the wide tile's halo: the wide look-ahead scan (records in the unit
+  // layout of the look-ahead scan for the same C)
+  constexpr int kNtA = kNtStore | kNtHalo;
+  if constexpr (sizeof(T) == 4 && C == 2) return launch_wide_ahead<T, A, C, 8, 1, kWG, kNtA, 0, 2, 4>(sg, k, st, ws, 1024);
+  if constexpr (sizeof(T) == 4 && C == 4) return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
+  if constexpr (sizeof(T) == 4 && C == 8) return launch_wide_ahead<T, A, C, 4, 1, 128, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
   (void)halo_bytes;
+  (void)ws;
   return MAVG_ERR_UNSUPPORTED;
 }
 
@@ -557,7 +637,7 @@ int dispatch_scan_c(bool vec, bool hs, const Sig& sg, int k, int block, hipStrea
   constexpr int VF = (C * (int)sizeof(T) <= 16 && 16 % (C * (int)sizeof(T)) == 0) ? 16 / (C * (int)sizeof(T)) : 0;
   if constexpr (sizeof(T) == 4 && (C == 2 || C == 4 || C == 8)) {
     if (vec && !hs && !sg.eio && block == 0) {
-      const int s = dispatch_wide<T, A, C>(sg, k, st);
+      const int s = dispatch_wide<T, A, C>(sg, k, st, ws);
       if (s != MAVG_ERR_UNSUPPORTED) return s;
     }
   }

@@ -4,6 +4,7 @@
 #pragma once
 
 #include "mavg_device.hpp"
+#include "mavg_lookback.hpp"
 
 namespace mavg {
 
@@ -72,11 +73,21 @@ __device__ __forceinline__ int out_slot(int g) {
   return g ^ ((g >> 3) & 7);
 }
 
-// extract elements [o, o + N) of a flat register array of N + EPG elements; o
-// uniform, one of the multiples of STEP below EPG (a chain of scalar compares)
-template <int O, int STEP, int EPG, typename T, int N>
-__device__ __forceinline__ void extract_chunk(const T (&flat)[N + EPG], T (&r)[N], int o) {
-  if constexpr (O + STEP >= EPG) {
+// the chunk's registers are raw dwords (a 16-B granule = 4 dwords): element
+// i of a chunk of T
+template <typename T>
+__device__ __forceinline__ T chunk_elem(const uint32_t* w, int i) {
+  if constexpr (sizeof(T) == 4) {
+    return __uint_as_float(w[i]);
+  } else {
+    return (T)(int16_t)(uint16_t)(w[i >> 1] >> (16 * (i & 1)));
+  }
+}
+// r[i] = flat[o + i] for a uniform dword offset o, one of the multiples of
+// STEP below 4 (a chain of scalar compares, one static copy taken)
+template <int O, int STEP, int N>
+__device__ __forceinline__ void shift_words(const uint32_t (&flat)[N + 4], uint32_t (&r)[N], int o) {
+  if constexpr (O + STEP >= 4) {
 #pragma unroll
     for (int i = 0; i < N; ++i) r[i] = flat[O + i];
   } else {
@@ -85,7 +96,7 @@ __device__ __forceinline__ void extract_chunk(const T (&flat)[N + EPG], T (&r)[N
       for (int i = 0; i < N; ++i) r[i] = flat[O + i];
       return;
     }
-    extract_chunk<O + STEP, STEP, EPG, T, N>(flat, r, o);
+    shift_words<O + STEP, STEP, N>(flat, r, o);
   }
 }
 
@@ -200,44 +211,41 @@ __global__ __launch_bounds__(WG) void wide_tile_kernel(WideParams p) {
   }
 
   // chunk j: x from the stage, and x[n-k] (an element shift of the same stage)
-  auto x_chunk = [&](int j, T (&xv)[CE]) {
-#pragma unroll
-    for (int i = 0; i < G; ++i) {
-      const Gr g = gread(Hg + j * G + i);
-#pragma unroll
-      for (int e = 0; e < EPG; ++e) xv[i * EPG + e] = g.e[e];
-    }
+  static_assert((C * sizeof(T)) % 4 == 0, "frames of whole dwords: x[n-k] shifts by whole dwords");
+  constexpr int NWD = G * 4;  // dwords per chunk
+  auto gwords = [&](int g, uint32_t* d) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(sb + stage_slot<QM>(g) * 16);
+    d[0] = v[0];
+    d[1] = v[1];
+    d[2] = v[2];
+    d[3] = v[3];
   };
-  auto xk_chunk = [&](int j, T (&xk)[CE]) {
+  auto x_chunk = [&](int j, uint32_t (&xv)[NWD]) {
+#pragma unroll
+    for (int i = 0; i < G; ++i) gwords(Hg + j * G + i, xv + 4 * i);
+  };
+  auto xk_chunk = [&](int j, uint32_t (&xk)[NWD]) {
     const int e = Hg * EPG + j * CE - k * C;  // stage element of x[n-k] for the chunk's first frame
     MAVG_DCHECK(e >= 0 && e + CE <= (Hg + TG) * EPG, "wide x[n-k] stage index", e, j);
-    if constexpr (C % EPG == 0) {
+    constexpr int kStep = C * (int)sizeof(T) / 4;  // dwords per frame
+    if constexpr (kStep % 4 == 0) {
 #pragma unroll
-      for (int i = 0; i < G; ++i) {
-        const Gr g = gread(e / EPG + i);
-#pragma unroll
-        for (int q = 0; q < EPG; ++q) xk[i * EPG + q] = g.e[q];
-      }
+      for (int i = 0; i < G; ++i) gwords(e / EPG + i, xk + 4 * i);
     } else {
       if (p.xk_off == 0) {
 #pragma unroll
-        for (int i = 0; i < G; ++i) {
-          const Gr g = gread(e / EPG + i);
-#pragma unroll
-          for (int q = 0; q < EPG; ++q) xk[i * EPG + q] = g.e[q];
-        }
+        for (int i = 0; i < G; ++i) gwords(e / EPG + i, xk + 4 * i);
       } else {
         const int gs = (e - p.xk_off) / EPG;
-        T flat[CE + EPG];
+        uint32_t flat[NWD + 4];
 #pragma unroll
-        for (int i = 0; i <= G; ++i) {
-          const Gr g = gread(gs + i);
-#pragma unroll
-          for (int q = 0; q < EPG; ++q) flat[i * EPG + q] = g.e[q];
-        }
-        extract_chunk<C, C, EPG, T, CE>(flat, xk, p.xk_off);
+        for (int i = 0; i <= G; ++i) gwords(gs + i, flat + 4 * i);
+        shift_words<kStep, kStep, NWD>(flat, xk, p.xk_off * (int)sizeof(T) / 4);
       }
     }
+  };
+  auto d_at = [&](const uint32_t (&xv)[NWD], const uint32_t (&xk)[NWD], int i) -> A {
+    return to_acc<A>(chunk_elem<T>(xv, i)) - to_acc<A>(chunk_elem<T>(xk, i));
   };
 
   // ---- pass 1: chunk totals, wave scans, segment totals ----
@@ -245,7 +253,7 @@ __global__ __launch_bounds__(WG) void wide_tile_kernel(WideParams p) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int j = u * WG + tid;
-    T xv[CE], xk[CE];
+    uint32_t xv[NWD], xk[NWD];
     x_chunk(j, xv);
     xk_chunk(j, xk);
     A run[C];
@@ -254,7 +262,7 @@ __global__ __launch_bounds__(WG) void wide_tile_kernel(WideParams p) {
 #pragma unroll
     for (int fr = 0; fr < P; ++fr)
 #pragma unroll
-      for (int c = 0; c < C; ++c) run[c] += to_acc<A>(xv[fr * C + c]) - to_acc<A>(xk[fr * C + c]);
+      for (int c = 0; c < C; ++c) run[c] += d_at(xv, xk, fr * C + c);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const A incl = wave_incl_scan(run[c]);
@@ -284,7 +292,7 @@ __global__ __launch_bounds__(WG) void wide_tile_kernel(WideParams p) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int j = u * WG + tid;
-    T xv[CE], xk[CE];
+    uint32_t xv[NWD], xk[NWD];
     x_chunk(j, xv);
     xk_chunk(j, xk);
     A run[C];
@@ -294,7 +302,7 @@ __global__ __launch_bounds__(WG) void wide_tile_kernel(WideParams p) {
     for (int fr = 0; fr < P; ++fr)
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        run[c] += to_acc<A>(xv[fr * C + c]) - to_acc<A>(xk[fr * C + c]);
+        run[c] += d_at(xv, xk, fr * C + c);
         yv[u][fr * C + c] = to_out<T, A, DV>(run[c], p.o);
       }
   }
@@ -337,6 +345,396 @@ __global__ __launch_bounds__(WG) void wide_tile_kernel(WideParams p) {
       const int s = r * 64 + lane;
       const Gr g = IO::load(reinterpret_cast<const T*>(rb + s * 16));
       IO::template store<(NT & kNtStore) != 0>(ob + out_slot(s) * EPG, g);
+    }
+  }
+}
+
+}  // namespace mavg
+
+namespace mavg {
+
+// ----------------------------------------------------------------------------
+// wide_ahead_kernel: the look-ahead scan (mavg_lookback.hpp) with the wide
+// in-tile scan, for multi-channel windows too long for the wide tile's
+// LDS-staged halo.  The record carry is the look-ahead scan's per-tile form,
+// unchanged and in its own unit layout (F frames per unit, U units per lane:
+// phase A of tile t + D, the own records of the first D slots, head duty,
+// bounded polling and the consumer's recompute -- the same bits whoever
+// computes a record); only the in-tile scan and the outputs change:
+//   - the tile itself and the shifted tile (its x[n-k]) reach two swizzled
+//     LDS stages by LDS-DMA (no tile registers);
+//   - lanes own chunks of P consecutive frames (mavg_wide.hpp), one wave scan
+//     per channel per chunk;
+//   - outputs leave through LDS as 1-KiB contiguous stores.
+// Per-wave records, run totals, self-publication and the Hillis-Steele form
+// stay in ahead_scan_kernel (mono / int16 paths).
+// ----------------------------------------------------------------------------
+template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U>
+__global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
+  constexpr int NW = WG / 64;
+  constexpr int EPG = 16 / (int)sizeof(T);
+  constexpr int CE = P * C;
+  constexpr int G = CE / EPG;
+  static_assert(CE % EPG == 0 && (G == 4 || G == 8), "64-B or 128-B chunks");
+  constexpr int QM = G == 4 ? 3 : 7;
+  constexpr int TF = WG * P * UW;
+  static_assert(TF == WG * F * U, "the record units tile the same frames as the chunks");
+  constexpr int TG = WG * UW * G;  // tile granules
+  constexpr int SG = TG + 1;       // shifted-tile granules (one more for an x[n-k] extraction)
+  constexpr int NSEG = UW * NW;
+  constexpr int VE = F * C;
+  using IO = UnitIO<T, VE>;
+  using GIO = UnitIO<T, EPG>;
+  using Gr = Unit<T, EPG>;
+  using SA = typename ScanAcc<T, A>::type;
+  constexpr int NG = GranCount<SA>::n;
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* sstage = smem;              // [SG] shifted tile, swizzled granules
+  unsigned char* tstage = smem + SG * 16;    // [TG] the tile, swizzled granules (then the outputs)
+  A* hsum = reinterpret_cast<A*>(tstage + TG * 16);  // [NW][C]
+  SA* tot = reinterpret_cast<SA*>(hsum + NW * C);    // [NSEG][C]
+  SA* shares = tot + NSEG * C;                         // [3][NW][C]
+
+  const T* __restrict__ in = static_cast<const T*>(p.in);
+  T* __restrict__ out = static_cast<T*>(p.out);
+  const T* __restrict__ hist = static_cast<const T*>(p.hist);
+  gran_t* gran = (gran_t*)p.gran;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int wq = __builtin_amdgcn_readfirstlane(w);
+  const int k = p.k;
+  const long long nframes = p.nframes;
+  const int pre = p.pre;
+
+  auto map_tile = [&](unsigned b) -> long long { return remap_tile(b, gridDim.x, p.xcd_remap); };
+  const long long tile = map_tile(blockIdx.x);
+  const long long t0 = tile * TF;
+  const int Ha = p.halo_units * F;  // the shifted stage starts Ha >= k frames before the tile
+  const long long h0 = t0 - Ha;
+  MAVG_DCHECK(tile >= 0 && tile < (long long)gridDim.x && t0 < nframes, "wide ahead tile index", tile, gridDim.x);
+  const bool tile_full = t0 + TF <= nframes;
+  const long long a = t0 - k;
+  const long long jlo = a >= 0 ? (a + TF - 1) / TF : 0;
+  const long long qlo = jlo, qhi = tile;  // per-tile records of the whole tiles [jlo, tile)
+  const int pcount = a >= 0 ? (int)(jlo * TF - a) : 0;
+  const long long nitem = qhi - qlo;
+
+  // ---- 1. the tile and the shifted tile to LDS; phase A; own / head-duty records ----
+  const unsigned nb = gridDim.x;
+  const unsigned bd = blockIdx.x + (unsigned)p.ahead;
+  const long long ja = bd < nb ? map_tile(bd) : -1;
+  const bool produce = ja >= 0 && ja < p.nfull;
+  if (tile_full) {
+    const T* src = in + t0 * C;
+#pragma unroll
+    for (int i = 0; i < UW * G; ++i) {
+      const int gl = stage_slot<QM>(i * WG + tid);
+      glds16<(NT & kNtLoad) != 0>(src + (long long)gl * EPG, tstage + (i * WG + wq * 64) * 16);
+    }
+  } else {
+#pragma unroll 1
+    for (int gl = tid; gl < TG; gl += WG) {
+      Gr u;
+#pragma unroll
+      for (int i = 0; i < EPG; ++i) {
+        const int e = gl * EPG + i;
+        u.e[i] = load_elem(in, hist, t0 + e / C, e % C, C, nframes, k, pre);
+      }
+      GIO::store(reinterpret_cast<T*>(tstage + stage_slot<QM>(gl) * 16), u);
+    }
+  }
+  const bool stage_fast = h0 >= 0 && (h0 * C + (long long)SG * EPG) <= nframes * C;
+  if (stage_fast) {
+    const T* src = in + h0 * C;
+    for (int j0 = 0; j0 < SG; j0 += WG) {
+      const int s = j0 + tid;
+      if (s < SG) glds16<(NT & kNtHalo) != 0>(src + (long long)stage_slot<QM>(s) * EPG, sstage + (j0 + wq * 64) * 16);
+    }
+  } else {
+#pragma unroll 1
+    for (int gl = tid; gl < SG; gl += WG) {
+      Gr u;
+#pragma unroll
+      for (int i = 0; i < EPG; ++i) {
+        const int e = gl * EPG + i;
+        u.e[i] = load_elem(in, hist, h0 + e / C, e % C, C, nframes, k, pre);
+      }
+      GIO::store(reinterpret_cast<T*>(sstage + stage_slot<QM>(gl) * 16), u);
+    }
+  }
+  auto share = [&](int src, const SA (&r)[C]) {
+    if (lane == 0) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) shares[(src * NW + w) * C + c] = r[c];
+    }
+  };
+  if (produce) {  // phase A: tile t + D, default policy (its own later loads hit L2)
+    Unit<T, VE> xa[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xa[u] = IO::gload(in + (ja * TF + (long long)(u * WG + tid) * F) * C, false);
+    SA r[C];
+    wave_record<T, SA, C, F, U>(xa, r);
+    share(0, r);
+  }
+  const bool own = blockIdx.x < (unsigned)p.ahead && tile < p.nfull;  // no block D slots earlier
+  if (own) {
+    SA r[C];
+    wave_record_lean<T, SA, C, F, U, WG>(in, tile, w, lane, false, r);
+    share(1, r);
+  }
+  long long jh = -1;
+  if (p.xcd_remap == 1) {
+    const unsigned xr = blockIdx.x & 7u, s = blockIdx.x >> 3;
+    if (xr >= 1u && s < (unsigned)p.head) {
+      const long long j = run_start(xr, nb) - p.head + s;
+      if (j >= 0 && j < p.nfull) jh = j;
+    }
+  }
+  if (jh >= 0) {
+    SA r[C];
+    wave_record_lean<T, SA, C, F, U, WG>(in, jh, w, lane, false, r);
+    share(2, r);
+  }
+  // the carry reads one (record, channel) pair per thread: slot s = q*C + c
+  // (C x fewer registers held across the scan than whole records per thread;
+  // WG is a multiple of C, so a thread's channel cc is the same every round)
+  const long long nslot = nitem * C;
+  const int cc = tid % C;
+  unsigned long long rv[NG];
+  auto slot_load = [&](long long sl, unsigned long long (&v)[NG]) {
+#pragma unroll
+    for (int h = 0; h < NG; ++h) v[h] = gran_load(gran + (qlo * C + sl) * NG + h);
+  };
+  MAVG_DCHECK(qhi <= p.nfull, "wide record read range", qhi, p.nfull);
+  if (tid < nslot) {
+    slot_load(tid, rv);
+  } else {
+#pragma unroll
+    for (int h = 0; h < NG; ++h) rv[h] = 0ull;
+  }
+  __syncthreads();
+  if (w < 3) {
+    const long long j = w == 0 ? (produce ? ja : -1) : (w == 1 ? (own ? tile : -1) : jh);
+    if (j >= 0) {
+      SA r[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        r[c] = shares[(w * NW) * C + c];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) r[c] += shares[(w * NW + i) * C + c];
+      }
+      publish_record<SA, C>(gran, j, r, lane);
+    }
+  }
+
+  // ---- 2. the partial window before frame 0 (history / peeled head) ----
+  A hp[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) hp[c] = (A)0;
+  if (a < 0 && (hist != nullptr || pre > 0)) {
+#pragma unroll 1
+    for (long long f = a + tid; f < 0; f += WG)
+#pragma unroll
+      for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(load_elem(in, hist, f, c, C, nframes, k, pre));
+  }
+
+  // ---- 3. the wide in-tile scan; the partial window [a, jlo T) is the x[n-k]
+  //         of the tile's first pcount frames ----
+  constexpr int NWD = G * 4;
+  static_assert((C * sizeof(T)) % 4 == 0, "frames of whole dwords");
+  auto gwords = [&](const unsigned char* base, int g, uint32_t* d) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(base + stage_slot<QM>(g) * 16);
+    d[0] = v[0];
+    d[1] = v[1];
+    d[2] = v[2];
+    d[3] = v[3];
+  };
+  auto x_chunk = [&](int j, uint32_t (&xv)[NWD]) {
+#pragma unroll
+    for (int i = 0; i < G; ++i) gwords(tstage, j * G + i, xv + 4 * i);
+  };
+  auto xk_chunk = [&](int j, uint32_t (&xk)[NWD]) {
+    const int e = (Ha - k) * C + j * CE;  // shifted-stage element of x[n-k] for the chunk's first frame
+    MAVG_DCHECK(e >= 0 && e + CE <= SG * EPG, "wide ahead x[n-k] stage index", e, j);
+    constexpr int kStep = C * (int)sizeof(T) / 4;
+    if constexpr (kStep % 4 == 0) {
+#pragma unroll
+      for (int i = 0; i < G; ++i) gwords(sstage, e / EPG + i, xk + 4 * i);
+    } else {
+      if (p.xk_off == 0) {
+#pragma unroll
+        for (int i = 0; i < G; ++i) gwords(sstage, e / EPG + i, xk + 4 * i);
+      } else {
+        const int gs = (e - p.xk_off) / EPG;
+        uint32_t flat[NWD + 4];
+#pragma unroll
+        for (int i = 0; i <= G; ++i) gwords(sstage, gs + i, flat + 4 * i);
+        shift_words<kStep, kStep, NWD>(flat, xk, p.xk_off * (int)sizeof(T) / 4);
+      }
+    }
+  };
+  SA lx[UW][C];
+#pragma unroll
+  for (int uw = 0; uw < UW; ++uw) {
+    const int j = uw * WG + tid;
+    uint32_t xv[NWD], xk[NWD];
+    x_chunk(j, xv);
+    xk_chunk(j, xk);
+    const int f0 = j * P;
+    if (f0 < pcount) {
+#pragma unroll
+      for (int fr = 0; fr < P; ++fr)
+        if (f0 + fr < pcount)
+#pragma unroll
+          for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(chunk_elem<T>(xk, fr * C + c));
+    }
+    SA run[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) run[c] = (SA)0;
+#pragma unroll
+    for (int fr = 0; fr < P; ++fr)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        run[c] += to_acc<SA>(chunk_elem<T>(xv, fr * C + c)) - to_acc<SA>(chunk_elem<T>(xk, fr * C + c));
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const SA incl = wave_incl_scan(run[c]);
+      lx[uw][c] = incl - run[c];
+      const SA segtot = readlane(incl, 63);
+      if (lane == 0) tot[(uw * NW + w) * C + c] = segtot;
+    }
+  }
+
+  // ---- 4. whole-tile carry from the records, WG (record, channel) slots per round ----
+  A hq = (A)0;  // channel cc
+#pragma unroll 1
+  for (long long sb0 = 0; sb0 < nslot; sb0 += WG) {
+    const long long sl = sb0 + tid;
+    const bool act = sl < nslot;
+    if (sb0 != 0) {
+      if (act) {
+        slot_load(sl, rv);
+      } else {
+#pragma unroll
+        for (int h = 0; h < NG; ++h) rv[h] = 0ull;
+      }
+    }
+    bool miss = false;
+#pragma unroll
+    for (int h = 0; h < NG; ++h) miss |= act && (rv[h] >> 32) != 1ull;
+#pragma unroll 1
+    for (int it = 0; __any(miss) && it < p.spin; ++it) {
+      __builtin_amdgcn_s_sleep(2);
+      if (miss) slot_load(sl, rv);
+      miss = false;
+#pragma unroll
+      for (int h = 0; h < NG; ++h) miss |= act && (rv[h] >> 32) != 1ull;
+    }
+    // still untagged: the wave recomputes each such record from the input with
+    // the producer's sequence, once per record for all the lanes of its channels
+    unsigned long long mask = __ballot(miss);
+#pragma unroll 1
+    while (mask != 0ull) {
+      const int l = __builtin_ctzll(mask);
+      const long long ql = __shfl(sl, l, 64) / C;
+      SA r[C];
+      tile_record_lean<T, SA, C, F, U, WG>(in, qlo + ql, lane, false, r);
+      const bool mine = miss && sl / C == ql;
+      if (mine) {
+        SA v = r[0];
+#pragma unroll
+        for (int c = 1; c < C; ++c)
+          if (cc == c) v = r[c];
+#pragma unroll
+        for (int h = 0; h < NG; ++h) rv[h] = kGranTag | gran_word(v, h);
+      }
+      mask &= ~__ballot(mine);
+    }
+    if (act) {
+      uint32_t wd[NG];
+#pragma unroll
+      for (int h = 0; h < NG; ++h) wd[h] = (uint32_t)rv[h];
+      hq += (A)gran_value<SA>(wd);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const A r = readlane(wave_incl_scan(hp[c] + (cc == c ? hq : (A)0)), 63);
+    if (lane == 0) hsum[w * C + c] = r;
+  }
+  __syncthreads();
+
+  // ---- 5. carry + earlier segments; pass 2 rebuilt from the stages; outputs ----
+  static_assert(NSEG <= 64, "segment totals are scanned across one wave");
+  A w0[C];
+  SA ex[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    w0[c] = (A)0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) w0[c] += hsum[i * C + c];
+    const SA tv = lane < NSEG ? tot[lane * C + c] : (SA)0;
+    ex[c] = wave_incl_scan(tv) - tv;
+  }
+  T yv[UW][CE];
+#pragma unroll
+  for (int uw = 0; uw < UW; ++uw) {
+    const int j = uw * WG + tid;
+    uint32_t xv[NWD], xk[NWD];
+    x_chunk(j, xv);
+    xk_chunk(j, xk);
+    A b[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) b[c] = w0[c] + (A)(readlane(ex[c], uw * NW + wq) + lx[uw][c]);
+    SA run[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) run[c] = (SA)0;
+#pragma unroll
+    for (int fr = 0; fr < P; ++fr)
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        run[c] += to_acc<SA>(chunk_elem<T>(xv, fr * C + c)) - to_acc<SA>(chunk_elem<T>(xk, fr * C + c));
+        yv[uw][fr * C + c] = to_out<T, A, DV>(b[c] + (A)run[c], p.o);
+      }
+  }
+  if (!tile_full) {
+#pragma unroll
+    for (int uw = 0; uw < UW; ++uw) {
+      const long long f = t0 + (long long)(uw * WG + tid) * P;
+#pragma unroll
+      for (int fr = 0; fr < P; ++fr)
+        if (f + fr < nframes)
+#pragma unroll
+          for (int c = 0; c < C; ++c) out[(f + fr) * C + c] = yv[uw][fr * C + c];
+    }
+    return;
+  }
+  __syncthreads();  // every read of the tile stage is done: it takes the outputs
+#pragma unroll
+  for (int uw = 0; uw < UW; ++uw) {
+    unsigned char* rb = tstage + ((uw * WG + wq * 64) * G) * 16;
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      Gr g;
+#pragma unroll
+      for (int e = 0; e < EPG; ++e) g.e[e] = yv[uw][i * EPG + e];
+      GIO::store(reinterpret_cast<T*>(rb + out_slot(lane * G + i) * 16), g);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int uw = 0; uw < UW; ++uw) {
+    const unsigned char* rb = tstage + ((uw * WG + wq * 64) * G) * 16;
+    T* ob = out + (t0 + (long long)(uw * WG + wq * 64) * P) * C;
+#pragma unroll
+    for (int r = 0; r < G; ++r) {
+      const int s = r * 64 + lane;
+      const Gr g = GIO::load(reinterpret_cast<const T*>(rb + s * 16));
+      GIO::template store<(NT & kNtStore) != 0>(ob + out_slot(s) * EPG, g);
     }
   }
 }

@@ -127,7 +127,7 @@ def test_plan_describes_launch_without_gpu():
     assert dsp.plan(1 << 30, 1024, channels=2).startswith("wide_tile<f32,acc=f64,C=2,P=16,U=1")
     assert dsp.plan(1 << 30, 1024, channels=4).startswith("wide_tile<f32,acc=f64,C=4,P=8,U=1")
     assert dsp.plan(1 << 30, 1024, channels=8).startswith("wide_tile<f32,acc=f64,C=8,P=4,U=1")
-    assert dsp.plan(1 << 30, 1025, channels=8).startswith("ahead_scan<f32,acc=f64,C=8,F=2")
+    assert dsp.plan(1 << 30, 1025, channels=8).startswith("wide_ahead<f32,acc=f64,C=8,P=4")
     assert dsp.plan(3 << 28, 1024, channels=3).startswith("tile_scan<f32")  # 12-B frames: frame units
     assert dsp.plan(1 << 30, 1024, channels=2, algo="hillis").startswith("tile_scan<")
     # int16 keeps the register-staged tiles (bench.py's timing, tools/tune/ab_libs.py)
@@ -145,6 +145,16 @@ def test_plan_describes_launch_without_gpu():
     assert dsp.plan(3 * 1000, 7, channels=3, dtype=dsp.I16, algo="blelloch").startswith("tile_scan<i16,acc=i32,C=3,F=1")
     with pytest.raises(dsp.MavgError):
         dsp.plan(10, 0)
+
+
+def test_longest_plan_is_not_truncated():
+    """The look-ahead plan with window-matched runs and run totals is the
+    longest; its trailing ws= field (tools/tune/ahead_trace.py reads it) must
+    be whole."""
+    import digital_signal_processsing_amd as dsp
+    p = dsp.plan(1 << 30, 4_000_000)
+    assert "runs=1" in p and re.search(r" ws=\d+$", p), p
+    assert 0 < int(p.split(" ws=")[1]) <= dsp.workspace_bytes(1 << 30, 4_000_000), p
 
 
 def test_workspace_only_for_ahead_scan():

@@ -286,8 +286,8 @@ def test_period_remap_very_long_windows_with_tail(oracle_mod, gpu, dtype, C, k, 
     plan = dsp.plan(1 << 30, k, C, code, algo)
     G = int(plan.split("remap=")[1].split()[0])
     tile = int(plan.split("tile_frames=")[1].split()[0])
-    assert plan.startswith("ahead_scan<") and G > 1, plan
-    assert ("runs=1" in plan) == (C <= 2 and algo == "auto" and k > 384 * tile), plan
+    assert _is_long(plan) and G > 1, plan
+    assert ("runs=1" in plan) == (C <= 2 and algo == "auto" and k > 384 * tile and plan.startswith("ahead_scan<")), plan
     frames = tile * max(3 * 8 * G + 37, k // tile + 8 * G + 37) + 5  # past one window, 3 periods, a ragged tail
     assert int(dsp.plan(frames * C, k, C, code, algo).split("remap=")[1].split()[0]) == G
     if dtype == "f32":
@@ -319,11 +319,11 @@ def test_many_channels_auto(oracle_mod, gpu):
 
 
 # ---------------------------------------------------------------------------
-# the long-window scans: the row-band scan (mavg_band.hpp: rows of k frames,
-# row-tile sums exchanged inside a band) where its geometry applies, else the
-# look-ahead scan (mavg_lookback.hpp: whole-tile records published inside the
-# launch)
-LONG_KERNELS = ("band_scan", "ahead_scan")
+# the long-window scans: the look-ahead scan (mavg_lookback.hpp: whole-tile
+# records published inside the launch) and, for multi-channel fp32 frames, the
+# wide look-ahead scan (mavg_wide.hpp: the same record carry, the wide in-tile
+# scan)
+LONG_KERNELS = ("ahead_scan", "wide_ahead")
 
 
 def _is_long(plan):
@@ -572,11 +572,17 @@ def _wide_windows(dsp, C):
     """Windows around every shape change of the wide tile (halo rows, tile
     length, the last window it takes) and a few inside each range."""
     n = 1 << 24
+
+    def shape(k):
+        p = dsp.plan(n, k, C, dsp.F32)
+        return p.split(" grid")[0] + p.split("block=")[1].split()[0]
     ks = {1, 2, 3, 7, 8, 9, 63, 64, 65}
-    for k in range(1, 9000):
-        if dsp.plan(n, k, C, dsp.F32) != dsp.plan(n, k + 1, C, dsp.F32):
+    row = 64 // C  # frames per 256-B LDS row of the staged halo
+    ks.update({row - 1, row, row + 1, 2 * row + 1, 5 * row - 1})
+    for k in range(2, 9000):  # (k = 1 is a copy)
+        if shape(k) != shape(k + 1):
             ks.update({k - 1, k, k + 1, k + 2})
-    tf = int(dsp.plan(n, 1, C, dsp.F32).split("tile_frames=")[1].split()[0])
+    tf = int(dsp.plan(n, 2, C, dsp.F32).split("tile_frames=")[1].split()[0])
     ks.update({tf - 1, tf, tf + 1})
     return sorted(k for k in ks if k >= 1)
 
@@ -598,7 +604,7 @@ def test_wide_tile_every_window_edge(oracle_mod, gpu, C):
         x = oracle_mod.synth_f32(frames * C, seed=k, dist=2)
         r = oracle_mod.check_synth_exact(_run(x, k, C, "blelloch", gpu), k, C, seed=k, dist=2, rtol=RTOL)
         assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, (k, plan, r)
-    assert any(p.startswith("wide_tile<") for p in seen) and any(p.startswith("ahead_scan<") for p in seen), seen
+    assert any(p.startswith("wide_tile<") for p in seen) and any(p.startswith("wide_ahead<") for p in seen), seen
 
 
 @pytest.mark.parametrize("C,k", [(2, 1), (2, 7), (2, 1023), (2, 1024), (2, 4096), (4, 1), (4, 255), (4, 1024),
@@ -638,15 +644,17 @@ def test_wide_tile_short_signals_history_and_views(oracle_mod, gpu, C, k):
 
 
 @pytest.mark.parametrize("C,k", [(4, 4097), (4, 44_100), (8, 1025), (8, 44_100), (2, 4097)])
-def test_f32_wide_units_past_the_wide_tile(oracle_mod, gpu, C, k):
-    """Past the wide tile's LDS-staged halo the look-ahead scan runs in 32-B
-    (C=4) or 64-B (C=8) units: rounding data against the exact sums, a view 16
-    B (C=8: 32 B) into an allocation, and the frame-unit form for comparison."""
+def test_f32_multichannel_long_windows_every_form(oracle_mod, gpu, C, k):
+    """Past the wide tile's LDS-staged halo (the wide look-ahead scan):
+    rounding data against the exact sums, a view 16 B (C=8: 32 B) into an
+    allocation, and the frame-unit form (blelloch_scalar: the look-ahead scan
+    in one-frame units) for comparison."""
     import digital_signal_processsing_amd as dsp
     import torch
     frames = 300_007
     plan = dsp.plan(frames * C, k, C, dsp.F32)
-    assert plan.startswith("ahead_scan<") and ((f",C={C},F=2," in plan) == (C != 2)), plan
+    assert plan.startswith("wide_ahead<"), plan
+    assert dsp.plan(frames * C, k, C, dsp.F32, "blelloch_scalar").startswith("ahead_scan<")
     x = oracle_mod.synth_f32(frames * C, seed=k, dist=2)
     r = oracle_mod.check_synth_exact(_run(x, k, C, "blelloch", gpu), k, C, seed=k, dist=2, rtol=RTOL)
     assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, (plan, r)
@@ -658,6 +666,58 @@ def test_f32_wide_units_past_the_wide_tile(oracle_mod, gpu, C, k):
     dsp.moving_average_into(xb[off:], yb[off:], k, C, "blelloch")
     assert_f32_close(yb[off:].cpu().numpy(), ref, f"k={k} view")
     assert_f32_close(_run(x, k, C, "blelloch_scalar", gpu), ref, f"k={k} scalar")
+
+
+@pytest.mark.parametrize("C,k", [(2, 4097), (2, 44_100), (4, 2049), (4, 20_000), (8, 1025), (8, 44_100),
+                                 (8, 700_000)])
+def test_wide_ahead_bitwise_whatever_the_schedule(oracle_mod, gpu, C, k):
+    """Multi-channel fp32 windows past the wide tile run the wide look-ahead
+    scan: rounding data (dist 2) within the bar against the exact window sums,
+    and bitwise the same output when every record is recomputed by its
+    consumer (spin 0), under the one-pass (slots 0) and minimal look-ahead
+    schedules (the debug build's schedule hook) as under the release build's
+    default schedule; ragged XCD runs and a ragged tail tile."""
+    import digital_signal_processsing_amd as dsp
+    frames = max(2_600_000 // C, 3 * k) + 12_345
+    plan = dsp.plan(frames * C, k, C, dsp.F32)
+    assert plan.startswith("wide_ahead<"), plan
+    x = oracle_mod.synth_f32(frames * C, seed=k + C, dist=2)
+    base = _run(x, k, C, "auto", gpu)
+    r = oracle_mod.check_synth_exact(base, k, C, seed=k + C, dist=2, rtol=RTOL)
+    assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, (plan, r)
+    for sched in ({}, {"spin": 0}, {"slots": 0}, {"slots": 8, "spin": 0}):
+        y = _with_schedule(sched, lambda lib: _run(x, k, C, "auto", gpu, library=lib))
+        assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), sched
+
+
+@pytest.mark.parametrize("C", [2, 4, 8])
+def test_wide_ahead_edges_history_views(oracle_mod, gpu, C):
+    """The wide look-ahead scan at windows one frame either side of whole
+    tiles (empty, one-frame and full partial windows), signals shorter than the
+    window, a history reaching before frame 0, and 16-B / 32-B offset views."""
+    import digital_signal_processsing_amd as dsp
+    import torch
+    T = int(dsp.plan(1 << 24, 50_000, C, dsp.F32).split("tile_frames=")[1].split()[0])
+    for k in (16 * T - 1, 16 * T, 16 * T + 1, 3 * T + 7):
+        for frames in (k // 3 + 1, 200_003):
+            plan = dsp.plan(frames * C, k, C, dsp.F32)
+            if not plan.startswith("wide_ahead<"):
+                continue
+            x = oracle_mod.synth_f32(frames * C, offset=k + frames, dist=1)
+            assert_f32_close(_run(x, k, C, "blelloch", gpu), oracle_mod.mavg_f32(x, k, C), f"k={k} frames={frames}")
+    k, frames, cut = 20_000, 120_000, 37_001
+    x = oracle_mod.synth_f32(frames * C, offset=5, dist=1)
+    full = oracle_mod.mavg_f32(x, k, C)
+    lo = max(0, cut - (k - 1))
+    hist = np.zeros((k - 1) * C, dtype=np.float32)
+    hist[(k - 1 - (cut - lo)) * C:] = x[lo * C: cut * C]
+    assert_f32_close(_run(x[cut * C:], k, C, "blelloch", gpu, history=hist), full[cut * C:], "history")
+    off = 8 if C == 8 else 4
+    xb = torch.zeros(frames * C + off, dtype=torch.float32, device=gpu)
+    xb[off:] = torch.from_numpy(x).to(gpu)
+    yb = torch.zeros_like(xb)
+    dsp.moving_average_into(xb[off:], yb[off:], k, C, "blelloch")
+    assert_f32_close(yb[off:].cpu().numpy(), full, f"view +{off * 4} B")
 
 
 @pytest.mark.parametrize("fill", [0xFF, "tags"])

@@ -9,9 +9,10 @@ shift || true
 for spec in "$@"; do
   IFS=: read -r k C <<< "$spec"
   echo "== wide_ab k=$k C=$C"
-  timeout -k 10 150 tools/tune/wide_ab 30 "$k" "$C" 6 > "$OUT/c${C}_k${k}.log" 2>&1
+  IFS=: read -r k C DT <<< "$spec"; DT=${DT:-f32}
+  timeout -k 10 150 tools/tune/wide_ab 30 "$k" "$C" 6 1 "$DT" > "$OUT/${DT}_c${C}_k${k}.log" 2>&1
   rc=$?
-  cat "$OUT/c${C}_k${k}.log"
+  cat "$OUT/${DT}_c${C}_k${k}.log"
   [ $rc -ne 0 ] && { echo "wide_ab rc=$rc: stopping"; exit $rc; }
 done
 exit 0

@@ -5,7 +5,7 @@
 // checked against the library's (|dy| <= 1e-6 |y|, fp64 sums in another order).
 //
 // build: make -C tools/tune wide_ab
-// run:   tools/tune/wide_ab <log2n> <k> <C> [rounds] [dist]
+// run:   tools/tune/wide_ab <log2n> <k> <C> [rounds] [dist] [f32|i16]
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -35,42 +35,92 @@ struct Var {
   std::vector<float> ms;
 };
 
-template <int C, int P, int U, int WG = 256>
+template <typename T, typename A, int C, int P, int U, int WG = 256, int DV = 0>
 void add1(std::vector<Var>& vs, const Sig& sg, int k) {
   constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
   char name[64];
-  snprintf(name, sizeof name, "wide P%d U%d %d ntS", P, U, WG);
-  vs.push_back({name, [=](hipStream_t s) { return launch_wide_tile<float, double, C, P, U, WG, kNtS>(sg, k, s); }, {}});
+  snprintf(name, sizeof name, "wide P%d U%d %d ntS dv%d", P, U, WG, DV);
+  vs.push_back({name, [=](hipStream_t s) { return launch_wide_tile<T, A, C, P, U, WG, kNtS, DV>(sg, k, s); }, {}});
 }
 
 // the round-3 unit kernels for the same C (tile_scan / ahead_scan, 32-B or 64-B units)
-template <int C, int F>
+template <typename T, typename A, int C, int F>
 void add_unit(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   char name[64];
   snprintf(name, sizeof name, "r03 units F=%d", F);
-  vs.push_back({name, [=](hipStream_t s) { return dispatch_scan_f<float, double, C, F, false>(sg, k, 0, s, ws); }, {}});
+  vs.push_back({name, [=](hipStream_t s) { return dispatch_scan_f<T, A, C, F, false>(sg, k, 0, s, ws); }, {}});
+}
+
+template <typename T, typename A, int C, int P, int UW, int WG, int F, int U, int DV = 0>
+void addA(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D = 1024) {
+  constexpr int kNtA = kNtStore | kNtHalo;
+  char name[80];
+  snprintf(name, sizeof name, "wahead P%d U%d %d F%d U%d D%d dv%d", P, UW, WG, F, U, D, DV);
+  vs.push_back({name, [=](hipStream_t s) { return launch_wide_ahead<T, A, C, P, UW, WG, kNtA, DV, F, U>(sg, k, s, ws, D); }, {}});
 }
 
 template <int C>
 void add_wide(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
+  using T = float;
+  using A = double;
+  if (k > 1024) {  // the look-ahead range: the unit look-ahead against the wide look-ahead shapes
+    add_unit<T, A, C, C == 2 ? 2 : 1>(vs, sg, k, ws);
+    if constexpr (C == 2) {
+      addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws);
+      addA<T, A, C, 16, 1, 256, 2, 8>(vs, sg, k, ws);
+      addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 512);
+    } else if constexpr (C == 4) {
+      addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws);
+      addA<T, A, C, 8, 1, 256, 1, 8>(vs, sg, k, ws);
+      addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws, 512);
+    } else {
+      addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws);
+      addA<T, A, C, 4, 1, 128, 1, 4>(vs, sg, k, ws);
+      addA<T, A, C, 2, 1, 256, 1, 2>(vs, sg, k, ws);
+      addA<T, A, C, 4, 1, 128, 1, 4>(vs, sg, k, ws, 512);
+    }
+    if (k > 4096) return;
+  }
   if constexpr (C == 2) {
-    add_unit<C, 2>(vs, sg, k, ws);
-    add1<C, 8, 1>(vs, sg, k);
-    add1<C, 8, 2>(vs, sg, k);
-    add1<C, 16, 1>(vs, sg, k);
-    add1<C, 16, 1, 128>(vs, sg, k);
+    add_unit<T, A, C, 2>(vs, sg, k, ws);
+    add1<T, A, C, 8, 1>(vs, sg, k);
+    add1<T, A, C, 8, 2>(vs, sg, k);
+    add1<T, A, C, 16, 1>(vs, sg, k);
+    add1<T, A, C, 16, 1, 128>(vs, sg, k);
   } else if constexpr (C == 4) {
-    add_unit<C, 2>(vs, sg, k, ws);
-    add1<C, 4, 2>(vs, sg, k);
-    add1<C, 8, 1>(vs, sg, k);
-    add1<C, 8, 2>(vs, sg, k);
-    add1<C, 8, 1, 128>(vs, sg, k);
+    add_unit<T, A, C, 2>(vs, sg, k, ws);
+    add1<T, A, C, 4, 2>(vs, sg, k);
+    add1<T, A, C, 8, 1>(vs, sg, k);
+    add1<T, A, C, 8, 2>(vs, sg, k);
+    add1<T, A, C, 8, 1, 128>(vs, sg, k);
   } else {
-    add_unit<C, 2>(vs, sg, k, ws);
-    add_unit<C, 1>(vs, sg, k, ws);
-    add1<C, 4, 1>(vs, sg, k);
-    add1<C, 4, 1, 128>(vs, sg, k);
-    add1<C, 4, 2, 128>(vs, sg, k);
+    add_unit<T, A, C, 2>(vs, sg, k, ws);
+    add_unit<T, A, C, 1>(vs, sg, k, ws);
+    add1<T, A, C, 4, 1>(vs, sg, k);
+    add1<T, A, C, 4, 1, 128>(vs, sg, k);
+    add1<T, A, C, 4, 2, 128>(vs, sg, k);
+  }
+}
+
+// int16 (the reference's PCM data path): int32 accumulators (k <= 65535)
+template <int C>
+void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
+  using T = int16_t;
+  using A = int32_t;
+  constexpr int VF = 16 / (2 * C);
+  add_unit<T, A, C, VF>(vs, sg, k, ws);
+  if constexpr (C == 2) {
+    add1<T, A, C, 16, 1, 256, 0>(vs, sg, k);
+    add1<T, A, C, 16, 1, 256, 1>(vs, sg, k);
+  } else if constexpr (C == 4) {
+    add1<T, A, C, 8, 1, 256, 0>(vs, sg, k);
+    add1<T, A, C, 16, 1, 256, 0>(vs, sg, k);
+    add1<T, A, C, 8, 2, 256, 0>(vs, sg, k);
+  } else {
+    add1<T, A, C, 4, 1, 256, 0>(vs, sg, k);
+    add1<T, A, C, 8, 1, 256, 0>(vs, sg, k);
+    add1<T, A, C, 4, 2, 256, 0>(vs, sg, k);
+    add1<T, A, C, 8, 1, 128, 0>(vs, sg, k);
   }
 }
 
@@ -80,43 +130,52 @@ int main(int argc, char** argv) {
   const int C = argc > 3 ? atoi(argv[3]) : 4;
   const int rounds = argc > 4 ? atoi(argv[4]) : 6;
   const int dist = argc > 5 ? atoi(argv[5]) : 1;
+  const bool i16 = argc > 6 && std::string(argv[6]) == "i16";
+  const int dt = i16 ? MAVG_I16 : MAVG_F32;
+  const int eb = i16 ? 2 : 4;
   const int steps = 10;
   const long long n = 1LL << lg;
-  float *x, *y, *yref;
-  CK(hipMalloc(&x, n * 4));
-  CK(hipMalloc(&y, n * 4));
-  CK(hipMalloc(&yref, n * 4));
+  void *x, *y, *yref;
+  CK(hipMalloc(&x, n * eb));
+  CK(hipMalloc(&y, n * eb));
+  CK(hipMalloc(&yref, n * eb));
   hipStream_t st;
   CK(hipStreamCreate(&st));
-  if (mavg_fill_synthetic(x, n, MAVG_F32, 0x5EED, 0, dist, st) != MAVG_OK) return 1;
+  if (mavg_fill_synthetic(x, n, dt, 0x5EED, 0, i16 ? 0 : dist, st) != MAVG_OK) return 1;
   size_t wsb = 0;
-  mavg_workspace_bytes(n, C, k, MAVG_F32, MAVG_ALGO_BLELLOCH, 0, &wsb);
+  mavg_workspace_bytes(n, C, k, dt, MAVG_ALGO_BLELLOCH, 0, &wsb);
   const size_t ws2 = std::max<size_t>(wsb, 256u << 20);  // also the r03 unit kernels' look-ahead records
   void* ws = nullptr;
   CK(hipMalloc(&ws, ws2));
   char plan[256];
-  mavg_plan(n, C, k, MAVG_F32, MAVG_ALGO_BLELLOCH, 0, plan, sizeof plan);
+  mavg_plan(n, C, k, dt, MAVG_ALGO_BLELLOCH, 0, plan, sizeof plan);
 
-  Sig sg{x, y, nullptr, n / C};
+  const Sig sg{x, y, nullptr, n / C};
   std::vector<Var> vs;
   vs.push_back({std::string("lib: ") + plan, [=](hipStream_t s) {
-                  return mavg_run(x, y, n, C, k, MAVG_F32, MAVG_ALGO_BLELLOCH, 0, nullptr, ws, wsb, s);
+                  return mavg_run(x, y, n, C, k, dt, MAVG_ALGO_BLELLOCH, 0, nullptr, ws, wsb, s);
                 }, {}});
-  vs.push_back({"copy", [=](hipStream_t s) { return mavg_stream_copy(x, y, n * 4, s); }, {}});
-  switch (C) {
-    case 2: add_wide<2>(vs, sg, k, Workspace{ws, ws2}); break;
-    case 4: add_wide<4>(vs, sg, k, Workspace{ws, ws2}); break;
-    case 8: add_wide<8>(vs, sg, k, Workspace{ws, ws2}); break;
+  vs.push_back({"copy", [=](hipStream_t s) { return mavg_stream_copy(x, y, n * eb, s); }, {}});
+  const Workspace w2{ws, ws2};
+  switch (C * (i16 ? -1 : 1)) {
+    case 2: add_wide<2>(vs, sg, k, w2); break;
+    case 4: add_wide<4>(vs, sg, k, w2); break;
+    case 8: add_wide<8>(vs, sg, k, w2); break;
+    case -2: add_wide_i16<2>(vs, sg, k, w2); break;
+    case -4: add_wide_i16<4>(vs, sg, k, w2); break;
+    case -8: add_wide_i16<8>(vs, sg, k, w2); break;
     default: fprintf(stderr, "C must be 2, 4 or 8\n"); return 1;
   }
   // reference output: the library
   if (vs[0].run(st) != MAVG_OK) return 1;
-  CK(hipMemcpyAsync(yref, y, n * 4, hipMemcpyDeviceToDevice, st));
+  CK(hipMemcpyAsync(yref, y, n * eb, hipMemcpyDeviceToDevice, st));
   CK(hipStreamSynchronize(st));
   std::vector<float> href(n), h(n);
-  CK(hipMemcpy(href.data(), yref, n * 4, hipMemcpyDeviceToHost));
+  std::vector<int16_t> sref(i16 ? n : 0), sh(i16 ? n : 0);
+  if (i16) CK(hipMemcpy(sref.data(), yref, n * eb, hipMemcpyDeviceToHost));
+  else CK(hipMemcpy(href.data(), yref, n * eb, hipMemcpyDeviceToHost));
   for (size_t v = 2; v < vs.size(); ++v) {
-    CK(hipMemsetAsync(y, 0xff, n * 4, st));
+    CK(hipMemsetAsync(y, 0xff, n * eb, st));
     const int rc = vs[v].run(st);
     CK(hipStreamSynchronize(st));
     if (rc != MAVG_OK) {
@@ -124,10 +183,15 @@ int main(int argc, char** argv) {
       vs[v].run = nullptr;
       continue;
     }
-    CK(hipMemcpy(h.data(), y, n * 4, hipMemcpyDeviceToHost));
     long long bad = 0;
     double worst = 0;
-    for (long long i = 0; i < n; ++i) {
+    if (i16) {  // bit-exact
+      CK(hipMemcpy(sh.data(), y, n * eb, hipMemcpyDeviceToHost));
+      for (long long i = 0; i < n; ++i) bad += sh[i] != sref[i];
+    } else {
+      CK(hipMemcpy(h.data(), y, n * eb, hipMemcpyDeviceToHost));
+    }
+    for (long long i = 0; !i16 && i < n; ++i) {
       const double r = href[i], d = std::fabs((double)h[i] - r);
       const double rel = d / std::max(std::fabs(r), 1e-30);
       if (!(d <= 1e-6 * std::fabs(r) || d == 0.0)) {
@@ -163,8 +227,8 @@ int main(int argc, char** argv) {
       }
     }
   }
-  printf("n=2^%d k=%d C=%d rounds=%d dist=%d (fraction of 8 TB/s, mean of per-launch events)\n", lg, k, C, rounds,
-         dist);
+  printf("n=2^%d k=%d C=%d %s rounds=%d dist=%d (fraction of 8 TB/s, mean of per-launch events)\n", lg, k, C,
+         i16 ? "i16" : "f32", rounds, dist);
   for (auto& v : vs) {
     if (v.ms.empty()) continue;
     double m = 0;
@@ -173,7 +237,8 @@ int main(int argc, char** argv) {
     std::vector<float> s = v.ms;
     std::sort(s.begin(), s.end());
     const double md = s[s.size() / 2];
-    printf("%-72s mean %.4f ms  %.4f   median %.4f\n", v.name.c_str(), m, 8.0 * n / (m * 1e-3) / 8e12, 8.0 * n / (md * 1e-3) / 8e12);
+    printf("%-72s mean %.4f ms  %.4f   median %.4f\n", v.name.c_str(), m, 2.0 * eb * n / (m * 1e-3) / 8e12,
+           2.0 * eb * n / (md * 1e-3) / 8e12);
   }
   return 0;
 }
