@@ -245,7 +245,7 @@ inline bool ahead_past_l2(long long k, int C, int elem, int TF) {
   return k * C * elem > (1LL << 21) && k >= 8LL * TF;
 }
 template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0, bool HS = false,
-          bool RUNS = false, int WG = kWG>
+          bool RUNS = false, int WG = kWG, bool LATEA = false>
 int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead, bool self = false) {
   constexpr int NW = WG / 64;
   const long long nframes = sg.nframes;
@@ -302,7 +302,7 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
 #endif
   const size_t need = rec_bytes + run_bytes + 16 + trace_bytes;
   size_t lds = kStageBytes + (size_t)NW * C * sizeof(A) + (size_t)(NSEG + 3 * NW) * C * sizeof(SA);
-  if (HS) lds = (lds + 15) / 16 * 16 + (size_t)U * WG * VE * sizeof(T);  // + the tile itself (HS)
+  if (HS || LATEA) lds = (lds + 15) / 16 * 16 + (size_t)U * WG * VE * sizeof(T);  // + the tile (HS) / phase A's tile
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
 #ifdef MAVG_AHEAD_LDS_MIN  // tuning builds: fewer workgroups per CU through a bigger LDS allocation
   lds = std::max<size_t>(lds, MAVG_AHEAD_LDS_MIN);
@@ -310,9 +310,10 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
              "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dma=%d,wrec=%d,dv=%d> grid=%lld block=%d lds=%zu "
-             "tile_frames=%d ahead=%d remap=%d%s%s ws=%zu",
+             "tile_frames=%d ahead=%d remap=%d%s%s%s ws=%zu",
              type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC, (int)DMA, (int)WREC, DV,
-             ntiles, WG, lds, TF, ahead, xcd_remap, RUNS ? " runs=1" : "", self ? " self=1" : "", need);
+             ntiles, WG, lds, TF, ahead, xcd_remap, RUNS ? " runs=1" : "", self ? " self=1" : "", LATEA ? " latea=1" : "",
+             need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -343,7 +344,7 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
 #ifdef MAVG_AHEAD_TRACE
   p.trace = reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(ws.ptr) + need - trace_bytes);
 #endif
-  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV, HS, RUNS, WG>), dim3((unsigned)ntiles),
+  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV, HS, RUNS, WG, LATEA>), dim3((unsigned)ntiles),
                      dim3(WG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
@@ -595,38 +596,61 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
   }
 }
 
-// The wide-frame tile scan (mavg_wide.hpp) for multi-channel fp32 frames
-// while its halo fits the LDS stage; MAVG_ERR_UNSUPPORTED otherwise (the
-// caller falls back to the unit kernels).  Shapes from the in-process A/B
-// against the round-3 unit kernels (tools/tune/wide_ab.hip, 2^30 samples,
-// fraction of 8 TB/s, profiles/r04_tuning/wide/):
-//   C=2  k=7 0.693 -> 0.790 (P8 U1), k=1024 0.645 -> 0.784, k=2048 0.649 ->
-//        0.781, k=4096 0.662 (look-ahead) -> 0.700 (P16 U1: 4096-frame tiles)
-//   C=4  k=7 0.651 -> 0.776, k=256 0.650 -> 0.794 (P8 U2), k=1024 0.506 ->
-//        0.774, k=2048 0.509 (look-ahead) -> 0.665 (P8 U1)
-//   C=8  k=7 0.416 -> 0.794 (P4 x 128 threads), k=256 0.259 -> 0.700, k=512
-//        0.237 -> 0.671, k=1024 0.234 -> 0.537 (P4 U1; 64 KiB of stage, two
-//        workgroups per CU)
+// The wide-frame kernels (mavg_wide.hpp) for multi-channel frames: the wide
+// tile while its halo fits the LDS stage, then the wide look-ahead scan;
+// MAVG_ERR_UNSUPPORTED where the unit kernels stay (the caller falls back).
+// Shapes from in-process A/Bs against the round-3 unit kernels
+// (tools/tune/wide_ab.hip, 2^30 samples, fraction of 8 TB/s, mean of
+// per-launch events; profiles/r04_tuning/wide/):
+//   fp32 C=2  k=7 0.693 -> 0.790 (P8 U1), k=1024 0.645 -> 0.784, k=2048 0.649
+//             -> 0.781, k=4096 0.662 -> 0.700 (P16 U1: 4096-frame tiles);
+//             look-ahead k=8192 0.646 -> 0.658, k=44100 0.636 -> 0.642 (D=512)
+//   fp32 C=4  k=7 0.651 -> 0.776, k=256 0.650 -> 0.794 (P8 U2), k=1024 0.506
+//             -> 0.774, k=2048 0.509 -> 0.665 (P8 U1); look-ahead k=4096
+//             0.515 -> 0.553, k=44100 ~0.48 -> 0.527 (P4, D=512)
+//   fp32 C=8  k=7 0.416 -> 0.794 (P4 x 128 threads), k=256 0.259 -> 0.700,
+//             k=512 0.237 -> 0.671, k=1024 0.234 -> 0.537 (P4 U1); look-ahead
+//             k=2048 0.236 -> 0.442 (128 threads, D=512), k=44100 0.180 ->
+//             0.378 (256 threads, D=1024)
+//   int16 C=4 k=7 0.689 -> 0.810 (P8 U1), k=1024 0.711 -> 0.770, k=2048 0.618
+//             -> 0.743 (P16 U1); int16 C=8 k=7 0.552 -> 0.798 (P8 x 128
+//             threads), k=1024 0.457 -> 0.722, k=2048 0.169 -> 0.591 (P8 U1),
+//             look-ahead k=44100 0.400 -> 0.476 (P4)
+//   The output division of the int16 wide kernels is the fp64 product (dv=0:
+//   int16 C=8 k=1024 P4 0.560 -> 0.602 against the magic multiply).
+//   Kept on the unit kernels: fp32 mono and int16 mono/stereo (a tie or a
+//   loss: int16 stereo k=1024 0.786 vs 0.788, k=44100 0.631 vs 0.587; fp32
+//   mono k=44100 0.677 vs 0.663).
 template <typename T, typename A, int C>
 int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
+  constexpr int kNtA = kNtStore | kNtHalo;
   const long long halo_bytes = (long long)k * C * (long long)sizeof(T);
   if constexpr (sizeof(T) == 4 && C == 2) {
     if (halo_bytes <= 2048) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 16, 1, kWG, kNtS>(sg, k, st);
+    return launch_wide_ahead<T, A, C, 8, 1, kWG, kNtA, 0, 2, 4>(sg, k, st, ws, 512);
   } else if constexpr (sizeof(T) == 4 && C == 4) {
     if (halo_bytes <= 4096) return launch_wide_tile<T, A, C, 8, 2, kWG, kNtS>(sg, k, st);
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
+    return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 512);
   } else if constexpr (sizeof(T) == 4 && C == 8) {
     if (halo_bytes <= 256) return launch_wide_tile<T, A, C, 4, 1, 128, kNtS>(sg, k, st);
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 4, 1, kWG, kNtS>(sg, k, st);
+    if (halo_bytes <= 131072) return launch_wide_ahead<T, A, C, 4, 1, 128, kNtA, 0, 1, 4>(sg, k, st, ws, 512);
+    return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
+  } else if constexpr (sizeof(T) == 2 && C == 4) {
+    if constexpr (sizeof(A) == 4) {
+      if (halo_bytes <= 8192) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
+      if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 16, 1, kWG, kNtS>(sg, k, st);
+    }
+  } else if constexpr (sizeof(T) == 2 && C == 8) {
+    if constexpr (sizeof(A) == 4) {
+      if (halo_bytes <= 256) return launch_wide_tile<T, A, C, 8, 1, 128, kNtS>(sg, k, st);
+      if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
+    }
+    return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
   }
-  // past the wide tile's halo: the wide look-ahead scan (records in the unit
-  // layout of the look-ahead scan for the same C)
-  constexpr int kNtA = kNtStore | kNtHalo;
-  if constexpr (sizeof(T) == 4 && C == 2) return launch_wide_ahead<T, A, C, 8, 1, kWG, kNtA, 0, 2, 4>(sg, k, st, ws, 1024);
-  if constexpr (sizeof(T) == 4 && C == 4) return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
-  if constexpr (sizeof(T) == 4 && C == 8) return launch_wide_ahead<T, A, C, 4, 1, 128, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
   (void)halo_bytes;
   (void)ws;
   return MAVG_ERR_UNSUPPORTED;
@@ -635,7 +659,7 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
 template <typename T, typename A, int C>
 int dispatch_scan_c(bool vec, bool hs, const Sig& sg, int k, int block, hipStream_t st, Workspace ws) {
   constexpr int VF = (C * (int)sizeof(T) <= 16 && 16 % (C * (int)sizeof(T)) == 0) ? 16 / (C * (int)sizeof(T)) : 0;
-  if constexpr (sizeof(T) == 4 && (C == 2 || C == 4 || C == 8)) {
+  if constexpr ((sizeof(T) == 4 && (C == 2 || C == 4 || C == 8)) || (sizeof(T) == 2 && (C == 4 || C == 8))) {
     if (vec && !hs && !sg.eio && block == 0) {
       const int s = dispatch_wide<T, A, C>(sg, k, st, ws);
       if (s != MAVG_ERR_UNSUPPORTED) return s;

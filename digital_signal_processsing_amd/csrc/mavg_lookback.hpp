@@ -364,11 +364,17 @@ __device__ __forceinline__ void run_total(const T* __restrict__ in, const gran_t
 #define MAVG_AHEAD_MINB_I16 1
 #endif
 template <typename T, typename A, int C, int F, int U, int NT, bool RC = false, bool DMA = true, bool WREC = false,
-          int DV = 0, bool HS = false, bool RUNS = false, int WG_ = kWG>
+          int DV = 0, bool HS = false, bool RUNS = false, int WG_ = kWG, bool LATEA = false>
 __global__ __launch_bounds__(WG_, RUNS ? MAVG_AHEAD_RUNS_MINB : (sizeof(T) == 4 ? MAVG_AHEAD_MINB_F32 : MAVG_AHEAD_MINB_I16))
 void ahead_scan_kernel(AheadParams p) {
   static_assert(!(HS && RC), "the Hillis-Steele flavour keeps its per-element prefixes");
   static_assert(!(RUNS && WREC), "run totals sum per-tile records");
+  // LATEA: phase A by LDS-DMA into a stage of its own, issued after the first
+  // barrier and summed after the in-tile scan, so its HBM latency overlaps the
+  // scan instead of preceding it, with no registers held across the scan;
+  // per-wave records only (each wave sums the part of the stage its own DMA
+  // filled: no barrier before publication)
+  static_assert(!LATEA || (WREC && !HS && !RUNS), "late phase A: per-wave records, Blelloch flavour");
   constexpr int WG = WG_;
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
@@ -389,7 +395,8 @@ void ahead_scan_kernel(AheadParams p) {
   A* hsum = reinterpret_cast<A*>(smem + kStageBytes);  // [NW][C] carry partials
   SA* tot = reinterpret_cast<SA*>(hsum + NW * C);       // [NSEG][C] segment totals
   SA* shares = tot + NSEG * C;                           // [3][NW][C] wave shares of the records published here
-  // HS: the tile itself, [U*WG] units, after the shares (16-B aligned)
+  // HS: the tile itself, [U*WG] units, after the shares (16-B aligned); LATEA:
+  // phase A's tile there instead
   T* tstage = reinterpret_cast<T*>(smem + ((kStageBytes + (NW * C * (int)sizeof(A)) +
                                             (NSEG + 3 * NW) * C * (int)sizeof(SA) + 15) & ~15));
 
@@ -463,13 +470,28 @@ void ahead_scan_kernel(AheadParams p) {
   const long long ja = bd < nb ? map_tile(bd) : -1;
   const bool produce = !p.self && ja >= 0 && ja < p.nfull;
   U_t xa[U];
-  if constexpr (WREC) {  // phase A's loads first: the HBM fetch with the longest latency
+  if constexpr (WREC && !LATEA) {  // phase A's loads first: the HBM fetch with the longest latency
     if (produce)
 #pragma unroll
       for (int u = 0; u < U; ++u) xa[u] = IO::gload(in + (ja * TF + (long long)(u * WG + tid) * F) * C, eio);
   }
+  // HS: whole tiles reach the tile stage by LDS-DMA (no tile registers, no
+  // ds_write; the scan reads the stage in its transposed order)
+#ifndef MAVG_HS_NODMA
+  constexpr bool kHsDma = HS && kDma;
+#else  // tuning builds: the round-3 register-staged HS tile (A/B)
+  constexpr bool kHsDma = false;
+#endif
+  const bool hs_dma = kHsDma && tile_full && !eio;
   U_t x[U];
-  if (tile_full) {
+  if (hs_dma) {
+    if constexpr (kHsDma) {
+      unsigned char* tb = reinterpret_cast<unsigned char*>(tstage);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        glds16<(NT & kNtLoad) != 0>(in + (t0 + (long long)(u * WG + tid) * F) * C, tb + (u * WG + wq * 64) * 16);
+    }
+  } else if (tile_full) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
       x[u] = IO::template gload<(NT & kNtLoad) != 0>(in + (t0 + (long long)(u * WG + tid) * F) * C, eio);
@@ -516,7 +538,7 @@ void ahead_scan_kernel(AheadParams p) {
       for (int c = 0; c < C; ++c) shares[(src * NW + w) * C + c] = r[c];
     }
   };
-  if (produce) {
+  if (produce && !LATEA) {
     if constexpr (!WREC)
 #pragma unroll
       for (int u = 0; u < U; ++u) xa[u] = IO::gload(in + (ja * TF + (long long)(u * WG + tid) * F) * C, eio);
@@ -528,7 +550,8 @@ void ahead_scan_kernel(AheadParams p) {
   const bool own = (p.self || blockIdx.x < (unsigned)p.ahead) && tile < p.nfull;  // no block D slots earlier
   if (own) {
     SA r[C];
-    wave_record<T, SA, C, F, U>(x, r);
+    if (hs_dma) wave_record_lean<T, SA, C, F, U, WG>(in, tile, w, lane, eio, r);  // rare: the first D slots
+    else wave_record<T, SA, C, F, U>(x, r);
     share(1, tile, r);
   }
   // head duty (remap mode 1): the first tiles of XCD run x need the records of
@@ -562,7 +585,7 @@ void ahead_scan_kernel(AheadParams p) {
   }
   if constexpr (HS) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) IO::store(tstage + (u * WG + tid) * VE, x[u]);
+    for (int u = 0; u < U && !hs_dma; ++u) IO::store(tstage + (u * WG + tid) * VE, x[u]);
   }
   __syncthreads();
   if (tid == 0) MAVG_ATRACE(2, MAVG_ANOW());  // first barrier
@@ -606,6 +629,18 @@ void ahead_scan_kernel(AheadParams p) {
           }
         }
       }
+    }
+  }
+
+  // LATEA: phase A's tile to its own stage now (default policy: the tile's own
+  // later loads hit L2); nothing waits for it before the in-tile scan is done
+  const bool late_a = LATEA && produce && !eio;
+  if constexpr (LATEA && kDma) {
+    if (late_a) {
+      unsigned char* ab = reinterpret_cast<unsigned char*>(tstage);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        glds16<false>(in + (ja * TF + (long long)(u * WG + tid) * F) * C, ab + (u * WG + wq * 64) * 16);
     }
   }
 
@@ -712,6 +747,32 @@ void ahead_scan_kernel(AheadParams p) {
       lx[u][c] = incl - run[c];
       const SA segtot = readlane(incl, 63);
       if (lane == 0) tot[(u * NW + w) * C + c] = segtot;
+    }
+  }
+
+  // LATEA: the wave's share of phase A's record from its own part of the stage
+  // (units u*WG + w*64 + lane: wave_record's order, the same bits), published
+  if constexpr (LATEA) {
+    if (produce) {
+      SA r[C];
+      if (late_a) {
+        SA ls[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) ls[c] = (SA)0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const U_t xu = IO::load(tstage + (u * WG + tid) * VE);
+#pragma unroll
+          for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+            for (int c = 0; c < C; ++c) ls[c] += to_acc<SA>(xu.e[fr * C + c]);
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) r[c] = readlane(wave_incl_scan(ls[c]), 63);
+      } else {  // element-aligned views: the record from global memory
+        wave_record_lean<T, SA, C, F, U, WG>(in, ja, w, lane, eio, r);
+      }
+      share(0, ja, r);
     }
   }
 

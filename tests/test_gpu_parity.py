@@ -568,21 +568,22 @@ def test_self_published_records(oracle_mod, gpu, k):
     assert_f32_close(_run(xf[cut:], k, 1, "blelloch", gpu, history=hist), full[cut:], f"k={k} history")
 
 
-def _wide_windows(dsp, C):
+def _wide_windows(dsp, C, dt=None):
     """Windows around every shape change of the wide tile (halo rows, tile
     length, the last window it takes) and a few inside each range."""
     n = 1 << 24
+    dt = dsp.F32 if dt is None else dt
 
     def shape(k):
-        p = dsp.plan(n, k, C, dsp.F32)
+        p = dsp.plan(n, k, C, dt)
         return p.split(" grid")[0] + p.split("block=")[1].split()[0]
     ks = {1, 2, 3, 7, 8, 9, 63, 64, 65}
-    row = 64 // C  # frames per 256-B LDS row of the staged halo
+    row = (64 if dt == dsp.F32 else 128) // C  # frames per 256-B LDS row of the staged halo
     ks.update({row - 1, row, row + 1, 2 * row + 1, 5 * row - 1})
     for k in range(2, 9000):  # (k = 1 is a copy)
         if shape(k) != shape(k + 1):
             ks.update({k - 1, k, k + 1, k + 2})
-    tf = int(dsp.plan(n, 2, C, dsp.F32).split("tile_frames=")[1].split()[0])
+    tf = int(dsp.plan(n, 2, C, dt).split("tile_frames=")[1].split()[0])
     ks.update({tf - 1, tf, tf + 1})
     return sorted(k for k in ks if k >= 1)
 
@@ -607,8 +608,29 @@ def test_wide_tile_every_window_edge(oracle_mod, gpu, C):
     assert any(p.startswith("wide_tile<") for p in seen) and any(p.startswith("wide_ahead<") for p in seen), seen
 
 
-@pytest.mark.parametrize("C,k", [(2, 1), (2, 7), (2, 1023), (2, 1024), (2, 4096), (4, 1), (4, 255), (4, 1024),
-                                 (4, 2048), (8, 1), (8, 8), (8, 9), (8, 1000), (8, 1024)])
+@pytest.mark.parametrize("C", [4, 8])
+def test_wide_int16_every_window_edge(oracle_mod, gpu, C):
+    """int16 with 4 and 8 channels runs the wide tile (and, C=8, the wide
+    look-ahead scan past it): bit-exact with the oracle at every window where
+    the plan changes, one frame either side, a ragged tail, with and without
+    a history."""
+    import digital_signal_processsing_amd as dsp
+    frames = 3 * 4096 + 1237
+    seen = set()
+    for k in _wide_windows(dsp, C, dsp.I16) + [20_000, 70_001]:
+        plan = dsp.plan(frames * C, k, C, dsp.I16)
+        seen.add(plan.split("<")[0])
+        x = oracle_mod.synth_i16((frames + k) * C, offset=k)
+        full = oracle_mod.mavg_i16(x, k, C)
+        assert np.array_equal(_run(x[: frames * C], k, C, "blelloch", gpu),
+                              oracle_mod.mavg_i16(x[: frames * C], k, C)), (k, plan)
+        y = _run(x[k * C:], k, C, "blelloch", gpu, history=x[C: k * C])
+        assert np.array_equal(y, full[k * C:]), (k, plan, "history")
+    assert "wide_tile" in seen and (("wide_ahead" in seen) == (C == 8)), seen
+
+
+@pytest.mark.parametrize("C,k", [(2, 2), (2, 7), (2, 1023), (2, 1024), (2, 4096), (4, 2), (4, 255), (4, 1024),
+                                 (4, 2048), (8, 2), (8, 8), (8, 9), (8, 1000), (8, 1024)])
 def test_wide_tile_short_signals_history_and_views(oracle_mod, gpu, C, k):
     """The wide tile's edge paths: signals shorter than a tile and than the
     window (every tile an edge tile), a history (the window reaching before

@@ -28,7 +28,8 @@ sys.path.insert(0, ROOT)
 
 TYPE = {"f32": "float", "f64": "double", "i16": "short", "i32": "int", "i64": "long"}
 FAMILY = {"tile_scan": "tile_scan_kernel", "direct": "direct_kernel",
-          "naive": "naive_kernel", "ahead_scan": "ahead_scan_kernel"}
+          "naive": "naive_kernel", "ahead_scan": "ahead_scan_kernel",
+          "wide_tile": "wide_tile_kernel", "wide_ahead": "wide_ahead_kernel"}
 
 
 def kernel_key(name):
@@ -58,6 +59,10 @@ def plan_key(plan):
         b = {"0": "false", "1": "true"}
         args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], b[kv["rc"]], b[kv["dma"]], b[kv["wrec"]], kv["dv"], hs,
                 "true" if " runs=1" in plan else "false", wg)
+    elif fam == "wide_tile":
+        args = (T, acc, kv["C"], kv["P"], kv["U"], wg, kv["nt"], kv.get("dv", "0"))
+    elif fam == "wide_ahead":
+        args = (T, acc, kv["C"], kv["P"], kv["U"], wg, kv["nt"], kv.get("dv", "0"), kv["F"], kv["FU"])
     else:
         args = (T, acc)
     return FAMILY[fam], args

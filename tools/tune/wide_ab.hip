@@ -60,10 +60,41 @@ void addA(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D = 1024
 }
 
 template <int C>
+void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws);
+
+// the look-ahead scan with phase A by LDS-DMA after the first barrier, summed
+// after the in-tile scan (LATEA; per-wave records)
+template <typename T, typename A, int C, int F, bool RC, bool LATE>
+void addL(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
+  constexpr int kNtA = kNtStore | kNtHalo;
+  char name[80];
+  snprintf(name, sizeof name, "ahead wrec D%d latea=%d", D, (int)LATE);
+  vs.push_back({name, [=](hipStream_t s) {
+                  return launch_ahead_scan<T, A, C, F, 4, kNtA, RC, true, true, 0, false, false, 256, LATE>(sg, k, s, ws, D);
+                }, {}});
+}
+
+template <int C>
 void add_wide(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   using T = float;
   using A = double;
-  if (k > 1024) {  // the look-ahead range: the unit look-ahead against the wide look-ahead shapes
+  if constexpr (C == 1) {  // mono long windows: the wide look-ahead against the tuned look-ahead
+    addL<T, A, C, 4, true, true>(vs, sg, k, ws, 512);
+    addL<T, A, C, 4, true, true>(vs, sg, k, ws, 1024);
+    addL<T, A, C, 4, true, false>(vs, sg, k, ws, 512);
+    addA<T, A, C, 16, 1, 256, 4, 4>(vs, sg, k, ws, 512);
+    addA<T, A, C, 16, 1, 256, 4, 4>(vs, sg, k, ws, 1024);
+    addA<T, A, C, 32, 1, 128, 4, 8>(vs, sg, k, ws, 512);
+  } else {
+    add_wide_c<C>(vs, sg, k, ws);
+  }
+}
+
+template <int C>
+void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
+  using T = float;
+  using A = double;
+  if (k > 1024 || (C == 8 && k == 1024)) {  // the look-ahead range: the unit look-ahead against the wide look-ahead shapes
     add_unit<T, A, C, C == 2 ? 2 : 1>(vs, sg, k, ws);
     if constexpr (C == 2) {
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws);
@@ -109,6 +140,21 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   using A = int32_t;
   constexpr int VF = 16 / (2 * C);
   add_unit<T, A, C, VF>(vs, sg, k, ws);
+  if (k > 8192) {  // the look-ahead range
+    if constexpr (C == 2) {
+      addL<T, A, C, 4, false, true>(vs, sg, k, ws, 768);
+      addL<T, A, C, 4, false, true>(vs, sg, k, ws, 1024);
+      addL<T, A, C, 4, false, false>(vs, sg, k, ws, 768);
+      addA<T, A, C, 16, 1, 256, 4, 4>(vs, sg, k, ws, 768);
+      addA<T, A, C, 16, 1, 256, 4, 4>(vs, sg, k, ws, 1024);
+    } else if constexpr (C == 4) {
+      addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 1024);
+    } else {
+      addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws, 1024);
+      addA<T, A, C, 8, 1, 256, 1, 8>(vs, sg, k, ws, 1024);
+    }
+    return;
+  }
   if constexpr (C == 2) {
     add1<T, A, C, 16, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 16, 1, 256, 1>(vs, sg, k);
@@ -158,13 +204,14 @@ int main(int argc, char** argv) {
   vs.push_back({"copy", [=](hipStream_t s) { return mavg_stream_copy(x, y, n * eb, s); }, {}});
   const Workspace w2{ws, ws2};
   switch (C * (i16 ? -1 : 1)) {
+    case 1: add_wide<1>(vs, sg, k, w2); break;
     case 2: add_wide<2>(vs, sg, k, w2); break;
     case 4: add_wide<4>(vs, sg, k, w2); break;
     case 8: add_wide<8>(vs, sg, k, w2); break;
     case -2: add_wide_i16<2>(vs, sg, k, w2); break;
     case -4: add_wide_i16<4>(vs, sg, k, w2); break;
     case -8: add_wide_i16<8>(vs, sg, k, w2); break;
-    default: fprintf(stderr, "C must be 2, 4 or 8\n"); return 1;
+    default: fprintf(stderr, "C must be 1, 2, 4 or 8\n"); return 1;
   }
   // reference output: the library
   if (vs[0].run(st) != MAVG_OK) return 1;
