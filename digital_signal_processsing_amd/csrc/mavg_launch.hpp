@@ -370,7 +370,7 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   constexpr int kNtA = kNtStore | kNtHalo;
   constexpr bool kRC = sizeof(T) == 4 && C == 1 && !HS;
   constexpr int D = C == 2 ? 768 : 1024;
-  int s;
+  int s = MAVG_ERR_UNSUPPORTED;
   // self-published records (AheadParams::self) for fp32 mono windows of at most 3 tiles: no phase A,
   // the records of the few tiles a window spans are out by the time the scan is done (A/B,
   // profiles/r03_tuning/self/: k=5000 0.704 -> 0.734, 8192 0.712 -> 0.735, 12288 0.709 -> 0.728;
@@ -380,8 +380,11 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
 #else
   const bool self = sizeof(T) == 4 && C == 1 && !HS && (long long)k <= 3LL * TF;
 #endif
-  if (C == 1 && (long long)k / TF + 1 <= 64)
-    s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true, 0, HS, false, WG>(sg, k, st, ws, 512, self);
+  // per-wave records: mono only (instantiated for C = 1 alone)
+  const bool wrec = C == 1 && (long long)k / TF + 1 <= 64;
+  if (wrec) {
+    if constexpr (C == 1) s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true, 0, HS, false, WG>(sg, k, st, ws, 512, self);
+  }
 #if !defined(MAVG_AHEAD_FIXED_RUN) && !defined(MAVG_AHEAD_NO_RUNS)
   // run totals (O(J + G) carry items instead of k/T) where the windows are
   // long enough to pay for the kernel's extra registers (4 waves per SIMD

@@ -175,6 +175,24 @@ __device__ __forceinline__ void publish_record(gran_t* gran, long long j, const 
   }
 }
 
+// The same publication from the NW wave shares of a record in LDS
+// (sh[i*C + c], wave i's share of channel c): each publishing lane adds its
+// own channel's shares in wave order (the bits of publish_record after the
+// same additions) -- an LDS address per lane instead of a register array
+// indexed by lane, which the compiler would move to scratch for C >= 4.
+template <typename SA, int C, int NW>
+__device__ __forceinline__ void publish_record_lds(gran_t* gran, long long j, const SA* sh, int lane) {
+  constexpr int NG = GranCount<SA>::n;
+  MAVG_DCHECK(j >= 0, "record index", j, lane);
+  if (lane < C * NG) {
+    const int c = lane / NG, h = lane - c * NG;
+    SA v = sh[c];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) v += sh[i * C + c];
+    gran_store(gran + (j * C + c) * NG + h, gran_word(v, h));
+  }
+}
+
 // first tile of XCD run x under remap mode 1 (remap_tile)
 __device__ __forceinline__ long long run_start(unsigned x, unsigned nb) {
   const unsigned q = nb >> 3, r = nb & 7u;
@@ -593,16 +611,7 @@ void ahead_scan_kernel(AheadParams p) {
   // source src's NW shares in wave order
   if (!WREC && w < 3) {
     const long long j = w == 0 ? (produce ? ja : -1) : (w == 1 ? (own ? tile : -1) : jh);
-    if (j >= 0) {
-      SA r[C];
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        r[c] = shares[(w * NW) * C + c];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) r[c] += shares[(w * NW + i) * C + c];
-      }
-      publish_record<SA, C>(gran, j, r, lane);
-    }
+    if (j >= 0) publish_record_lds<SA, C, NW>(gran, j, shares + (w * NW) * C, lane);
   }
   if constexpr (RUNS) {
     // run totals: wave 3 for the record published from phase A, wave 2 for

@@ -517,16 +517,7 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
   __syncthreads();
   if (w < 3) {
     const long long j = w == 0 ? (produce ? ja : -1) : (w == 1 ? (own ? tile : -1) : jh);
-    if (j >= 0) {
-      SA r[C];
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        r[c] = shares[(w * NW) * C + c];
-#pragma unroll
-        for (int i = 1; i < NW; ++i) r[c] += shares[(w * NW + i) * C + c];
-      }
-      publish_record<SA, C>(gran, j, r, lane);
-    }
+    if (j >= 0) publish_record_lds<SA, C, NW>(gran, j, shares + (w * NW) * C, lane);
   }
 
   // ---- 2. the partial window before frame 0 (history / peeled head) ----
