@@ -58,7 +58,7 @@ def plan_key(plan):
     elif fam == "ahead_scan":
         b = {"0": "false", "1": "true"}
         args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], b[kv["rc"]], b[kv["dma"]], b[kv["wrec"]], kv["dv"], hs,
-                "true" if " runs=1" in plan else "false", wg)
+                "true" if " runs=1" in plan else "false", wg, "true" if " latea=1" in plan else "false")
     elif fam == "wide_tile":
         args = (T, acc, kv["C"], kv["P"], kv["U"], wg, kv["nt"], kv.get("dv", "0"))
     elif fam == "wide_ahead":
