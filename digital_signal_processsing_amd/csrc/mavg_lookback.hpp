@@ -765,6 +765,10 @@ void ahead_scan_kernel(AheadParams p) {
     if (produce) {
       SA r[C];
       if (late_a) {
+        // the LDS-DMA writes count on vmcnt and the compiler does not order
+        // this wave's reads of its own DMA destination after them: wait here
+        // (every other vector-memory load of the tile is consumed by now)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         SA ls[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) ls[c] = (SA)0;
