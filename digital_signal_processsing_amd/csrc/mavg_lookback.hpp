@@ -382,8 +382,9 @@ __device__ __forceinline__ void run_total(const T* __restrict__ in, const gran_t
 #define MAVG_AHEAD_MINB_I16 1
 #endif
 template <typename T, typename A, int C, int F, int U, int NT, bool RC = false, bool DMA = true, bool WREC = false,
-          int DV = 0, bool HS = false, bool RUNS = false, int WG_ = kWG, bool LATEA = false>
-__global__ __launch_bounds__(WG_, RUNS ? MAVG_AHEAD_RUNS_MINB : (sizeof(T) == 4 ? MAVG_AHEAD_MINB_F32 : MAVG_AHEAD_MINB_I16))
+          int DV = 0, bool HS = false, bool RUNS = false, int WG_ = kWG, bool LATEA = false, bool PW = false>
+__global__ __launch_bounds__(WG_ + (PW ? 64 : 0),
+                             RUNS ? MAVG_AHEAD_RUNS_MINB : (sizeof(T) == 4 ? MAVG_AHEAD_MINB_F32 : MAVG_AHEAD_MINB_I16))
 void ahead_scan_kernel(AheadParams p) {
   static_assert(!(HS && RC), "the Hillis-Steele flavour keeps its per-element prefixes");
   static_assert(!(RUNS && WREC), "run totals sum per-tile records");
@@ -393,6 +394,13 @@ void ahead_scan_kernel(AheadParams p) {
   // per-wave records only (each wave sums the part of the stage its own DMA
   // filled: no barrier before publication)
   static_assert(!LATEA || (WREC && !HS && !RUNS), "late phase A: per-wave records, Blelloch flavour");
+  // PW: phase A in a producer wave of its own (the block's wave NW, after the
+  // NW scan waves): it issues the loads of tile t + D first thing, passes both
+  // block barriers without waiting for them, and sums and publishes the
+  // record(s) after the second barrier, so the scan waves never wait on the
+  // HBM fetch (their own loads are the L2 hits an earlier producer left).
+  // The records are the same sequences as wave_record / publish_record_lds.
+  static_assert(!(PW && LATEA), "one place for phase A");
   constexpr int WG = WG_;
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
@@ -486,7 +494,76 @@ void ahead_scan_kernel(AheadParams p) {
   const unsigned nb = gridDim.x;
   const unsigned bd = blockIdx.x + (unsigned)p.ahead;  // the block D dispatch slots later (same XCD)
   const long long ja = bd < nb ? map_tile(bd) : -1;
-  const bool produce = !p.self && ja >= 0 && ja < p.nfull;
+  const bool produce_any = !p.self && ja >= 0 && ja < p.nfull;
+  if constexpr (PW) {
+    if (wq == NW) {  // the producer wave
+      U_t xa[U * NW];  // slot i = wv * U + u: unit u * WG + wv * 64 + lane
+      if (produce_any)
+#pragma unroll
+        for (int i = 0; i < U * NW; ++i)
+          xa[i] = IO::gload(in + (ja * TF + (long long)((i % U) * WG + (i / U) * 64 + lane) * F) * C, eio);
+      // the block's two barriers, passed with the loads in flight (this wave
+      // shares nothing through LDS)
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_barrier();
+      if (!produce_any) return;
+      // the loaded values enter the sums only from here: an empty asm that
+      // "rewrites" each loaded dword keeps the compiler from hoisting the
+      // conversions (and the wait for the loads) above the barriers
+#pragma unroll
+      for (int i = 0; i < U * NW; ++i) {
+        static_assert(sizeof(U_t) % 4 == 0, "units of whole dwords");
+        uint32_t dw[sizeof(U_t) / 4];
+        __builtin_memcpy(dw, &xa[i], sizeof(U_t));
+#pragma unroll
+        for (int d = 0; d < (int)(sizeof(U_t) / 4); ++d) asm volatile("" : "+v"(dw[d]));
+        __builtin_memcpy(&xa[i], dw, sizeof(U_t));
+      }
+      SA rec[C];
+#pragma unroll
+      for (int wv = 0; wv < NW; ++wv) {
+        SA ls[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) ls[c] = (SA)0;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int fr = 0; fr < F; ++fr)
+#pragma unroll
+            for (int c = 0; c < C; ++c) ls[c] += to_acc<SA>(xa[wv * U + u].e[fr * C + c]);
+        SA r[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) r[c] = readlane(wave_incl_scan(ls[c]), 63);
+        if constexpr (WREC) {
+          publish_record<SA, C>(gran, ja * NW + wv, r, lane);
+        } else {
+#pragma unroll
+          for (int c = 0; c < C; ++c) rec[c] = wv == 0 ? r[c] : rec[c] + r[c];
+        }
+      }
+      if constexpr (!WREC) publish_record<SA, C>(gran, ja, rec, lane);
+      if constexpr (RUNS) {  // the run total that comes with this record (as wave 3 below)
+        const long long G = p.xcd_remap;
+        if ((ja + 1) % G == 0) {
+          const long long rr = (ja + 1) / G - 1 - 8;
+          if (rr >= 0 && rr < p.runs_done) {
+            A tt[C];
+            run_total<T, A, C, F, U, WG>(in, gran, rr * G, (int)G, p.spin, lane, eio, tt, p.stats);
+            if (lane < C * NGA) {
+              const int c = lane / NGA, h = lane - c * NGA;
+              A v = tt[0];
+#pragma unroll
+              for (int i = 1; i < C; ++i)
+                if (c == i) v = tt[i];
+              gran_store((gran_t*)p.runs + (rr * C + c) * NGA + h, gran_word(v, h));
+            }
+          }
+        }
+      }
+      return;
+    }
+  }
+  const bool produce = produce_any && !PW;  // phase A by the scan waves
   U_t xa[U];
   if constexpr (WREC && !LATEA) {  // phase A's loads first: the HBM fetch with the longest latency
     if (produce)

@@ -238,13 +238,6 @@ int run(int lg, int k, int rounds) {
 // variant lists (macros expand to launches of the library's launch helpers)
 template <>
 void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, long long n, int k) {
-#define SCAN(U, PD, NT, OV)                                                                                  \
-  vs.push_back({"scan U" #U " PD" #PD " NT" #NT " ov" #OV, true, [=](hipStream_t s) {                       \
-                  ScanTuning t;                                                                             \
-                  t.oversub = OV;                                                                           \
-                  return launch_scan<float, double, 1, 4, U, false, PD, NT>(Sig{x, y, nullptr, n}, k, s, t);     \
-                }});
-  SCAN(2, 2, 3, 1)
 #define TILE(U, NT, RM)                                                                                  \
   vs.push_back({"tile U" #U " NT" #NT " remap" #RM, true, [=](hipStream_t s) {                             \
                   return launch_tile_scan<float, double, 1, 4, U, false, NT>(Sig{x, y, nullptr, n}, k, s, RM);   \
@@ -256,13 +249,6 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
 #define TILEW(U, WG)                                                                                    \
   vs.push_back({"tile U" #U " wg" #WG, true, [=](hipStream_t s) {                                         \
                   return launch_tile_scan<float, double, 1, 4, U, false, 0, WG>(Sig{x, y, nullptr, n}, k, s, 1); \
-                }});
-#define SEGR(U, PD, NT, SC)                                                                              \
-  vs.push_back({"seg U" #U " PD" #PD " NT" #NT " sc" #SC " remap", true, [=](hipStream_t s) {              \
-                  ScanTuning t;                                                                         \
-                  t.seg_chunks = SC;                                                                    \
-                  t.xcd_remap = 1;                                                                      \
-                  return launch_scan<float, double, 1, 4, U, false, PD, NT>(Sig{x, y, nullptr, n}, k, s, t); \
                 }});
 #define TILEM(U, M)                                                                                     \
   vs.push_back({"tile U" #U " remap" #M, true, [=](hipStream_t s) {                                       \
@@ -385,12 +371,6 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   TILE(4, 3, 64)
   TILE(8, 0, 64)
   TILE(8, 3, 64)
-  vs.push_back({"seg rule", true, [=](hipStream_t s) {
-                  ScanTuning t;
-                  t.xcd_remap = 1;
-                  t.seg_chunks = std::max(4, 4 * ((k - 1 + 2047) / 2048));
-                  return launch_scan<float, double, 1, 4, 2, false, 2, 0>(Sig{x, y, nullptr, n}, k, s, t);
-                }});
   vs.push_back({"f32 product mavg_run", true, [=](hipStream_t s) {
                   return mavg_run(x, y, n, 1, k, MAVG_F32, MAVG_ALGO_AUTO, 0, nullptr, g_ws.ptr, g_ws.bytes, s);
                 }});
@@ -426,7 +406,6 @@ void add_variants<float, double>(std::vector<Variant>& vs, float* x, float* y, l
   DIRECTM(16)
   DIRECTM(64)
   DIRECTM(256)
-  SEGR(2, 2, 0, 4)
 
 }
 
@@ -542,12 +521,6 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
     STILE(4, 3, 64)
     STILE(8, 0, 64)
     STILE(8, 3, 64)
-    vs.push_back({"i16 stereo seg rule", true, [=](hipStream_t s) {
-                    ScanTuning t;
-                    t.xcd_remap = 1;
-                    t.seg_chunks = std::max(4, 4 * ((k - 1 + 2047) / 2048));
-                    return launch_scan<int16_t, int32_t, 2, 4, 2, false, 2, 0>(Sig{x, y, nullptr, n / 2}, k, s, t);
-                  }});
     return;
   }
 #define ITILEWG(U, WG, RC)                                                                              \
@@ -640,12 +613,6 @@ void add_variants<int16_t, int32_t>(std::vector<Variant>& vs, int16_t* x, int16_
   ITILENTR(4, 3, 64)
   ITILENTR(8, 0, 64)
   ITILENTR(8, 3, 64)
-  vs.push_back({"i16 seg rule", true, [=](hipStream_t s) {
-                  ScanTuning t;
-                  t.xcd_remap = 1;
-                  t.seg_chunks = std::max(4, 4 * ((k - 1 + 4095) / 4096));
-                  return launch_scan<int16_t, int32_t, 1, 8, 2, false, 2, 0>(Sig{x, y, nullptr, n}, k, s, t);
-                }});
   IPROD()
   if (k <= 64) {
     IDIRECT(1)

@@ -64,13 +64,14 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws);
 
 // the look-ahead scan with phase A by LDS-DMA after the first barrier, summed
 // after the in-tile scan (LATEA; per-wave records)
-template <typename T, typename A, int C, int F, bool RC, bool LATE>
+template <typename T, typename A, int C, int F, bool RC, bool LATE, bool PW = false, bool WREC = true>
 void addL(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
   constexpr int kNtA = kNtStore | kNtHalo;
   char name[80];
-  snprintf(name, sizeof name, "ahead wrec D%d latea=%d", D, (int)LATE);
+  snprintf(name, sizeof name, "ahead wrec=%d D%d latea=%d pw=%d", (int)WREC, D, (int)LATE, (int)PW);
   vs.push_back({name, [=](hipStream_t s) {
-                  return launch_ahead_scan<T, A, C, F, 4, kNtA, RC, true, true, 0, false, false, 256, LATE>(sg, k, s, ws, D);
+                  return launch_ahead_scan<T, A, C, F, 4, kNtA, RC, true, WREC, 0, false, false, 256, LATE, PW>(sg, k, s,
+                                                                                                                ws, D);
                 }, {}});
 }
 
@@ -80,11 +81,10 @@ void add_wide(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   using A = double;
   if constexpr (C == 1) {  // mono long windows: the wide look-ahead against the tuned look-ahead
     addL<T, A, C, 4, true, true>(vs, sg, k, ws, 512);
-    addL<T, A, C, 4, true, true>(vs, sg, k, ws, 1024);
     addL<T, A, C, 4, true, false>(vs, sg, k, ws, 512);
-    addA<T, A, C, 16, 1, 256, 4, 4>(vs, sg, k, ws, 512);
-    addA<T, A, C, 16, 1, 256, 4, 4>(vs, sg, k, ws, 1024);
-    addA<T, A, C, 32, 1, 128, 4, 8>(vs, sg, k, ws, 512);
+    addL<T, A, C, 4, true, false, true>(vs, sg, k, ws, 512);
+    addL<T, A, C, 4, true, false, true>(vs, sg, k, ws, 768);
+    addL<T, A, C, 4, true, false, true, false>(vs, sg, k, ws, 1024);
   } else {
     add_wide_c<C>(vs, sg, k, ws);
   }
@@ -141,12 +141,16 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   constexpr int VF = 16 / (2 * C);
   add_unit<T, A, C, VF>(vs, sg, k, ws);
   if (k > 8192) {  // the look-ahead range
-    if constexpr (C == 2) {
-      addL<T, A, C, 4, false, true>(vs, sg, k, ws, 768);
-      addL<T, A, C, 4, false, true>(vs, sg, k, ws, 1024);
-      addL<T, A, C, 4, false, false>(vs, sg, k, ws, 768);
-      addA<T, A, C, 16, 1, 256, 4, 4>(vs, sg, k, ws, 768);
-      addA<T, A, C, 16, 1, 256, 4, 4>(vs, sg, k, ws, 1024);
+    if constexpr (C == 1) {  // mono: per-wave records, D = 512 (the library's dispatch)
+      addL<T, A, C, 8, false, false, false, true>(vs, sg, k, ws, 512);
+      addL<T, A, C, 8, false, false, true, true>(vs, sg, k, ws, 512);
+      addL<T, A, C, 8, false, false, true, true>(vs, sg, k, ws, 768);
+      addL<T, A, C, 8, false, false, true, false>(vs, sg, k, ws, 1024);
+    } else if constexpr (C == 2) {
+      addL<T, A, C, 4, false, false, false, false>(vs, sg, k, ws, 768);
+      addL<T, A, C, 4, false, false, true, false>(vs, sg, k, ws, 768);
+      addL<T, A, C, 4, false, false, true, false>(vs, sg, k, ws, 1024);
+      addL<T, A, C, 4, false, false, true, false>(vs, sg, k, ws, 512);
     } else if constexpr (C == 4) {
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 1024);
     } else {
@@ -162,7 +166,7 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     add1<T, A, C, 8, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 16, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 8, 2, 256, 0>(vs, sg, k);
-  } else {
+  } else if constexpr (C == 8) {
     add1<T, A, C, 4, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 8, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 4, 2, 256, 0>(vs, sg, k);
@@ -208,6 +212,7 @@ int main(int argc, char** argv) {
     case 2: add_wide<2>(vs, sg, k, w2); break;
     case 4: add_wide<4>(vs, sg, k, w2); break;
     case 8: add_wide<8>(vs, sg, k, w2); break;
+    case -1: add_wide_i16<1>(vs, sg, k, w2); break;
     case -2: add_wide_i16<2>(vs, sg, k, w2); break;
     case -4: add_wide_i16<4>(vs, sg, k, w2); break;
     case -8: add_wide_i16<8>(vs, sg, k, w2); break;
