@@ -241,11 +241,14 @@ inline int ahead_run_length(long long k, int TF, int ahead) {
 // ahead: D, the dispatch slots between a record's producer and its tile (a
 // multiple of 8; the test hook overrides it)
 // Windows past an XCD's L2 reach run in window-matched runs (remap mode G)
+// fp32 mono 8192-frame look-ahead tiles up to this many tiles per window
+// (beyond: the 4096-frame run-total kernel)
+constexpr long long kAheadU8MaxTiles = 1024;
 inline bool ahead_past_l2(long long k, int C, int elem, int TF) {
   return k * C * elem > (1LL << 21) && k >= 8LL * TF;
 }
 template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0, bool HS = false,
-          bool RUNS = false, int WG = kWG, bool LATEA = false, bool PW = false>
+          bool RUNS = false, int WG = kWG, bool LATEA = false, int PW = 0>
 int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead, bool self = false) {
   constexpr int NW = WG / 64;
   const long long nframes = sg.nframes;
@@ -313,7 +316,7 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
              "tile_frames=%d ahead=%d remap=%d%s%s%s%s ws=%zu",
              type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC, (int)DMA, (int)WREC, DV,
              ntiles, WG, lds, TF, ahead, xcd_remap, RUNS ? " runs=1" : "", self ? " self=1" : "", LATEA ? " latea=1" : "",
-             PW ? " pw=1" : "", need);
+             PW == 1 ? " pw=1" : PW == 2 ? " pw=2" : "", need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -380,6 +383,32 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
 #else
   const bool self = sizeof(T) == 4 && C == 1 && !HS && (long long)k <= 3LL * TF;
 #endif
+  // 8192-frame tiles (U = 8, 32 KiB) with per-tile records: 3 workgroups per
+  // CU with twice the bytes each instead of 5-6 with 16 KiB, and a shorter
+  // look-ahead in slots (fp32 D = 320, int16 D = 256) for about the same
+  // prefetch in bytes.  Kept where bench.py's timing shows the gain
+  // (tools/tune/ab_libs.py against -DMAVG_AHEAD_NO_U8, profiles/r04_tuning/u8/):
+  //   fp32 mono past the L2 reach (window-matched runs), up to 1024 tiles,
+  //     without run totals: k=2e6 0.613 -> 0.650, 4e6 0.589 -> 0.621, 1e6
+  //     0.657 -> 0.660; shorter fp32 windows lose (k=44100 0.703 -> 0.684,
+  //     20000 0.690 -> 0.674) and keep the 4096-frame per-wave records;
+  //   int16 stereo short of the run-total range: k=44100 0.629 -> 0.643,
+  //     1e5 0.527 -> 0.572.
+  //   int16 mono (16384-frame tiles) lost in the tuner (0.680 -> 0.667).
+  // (16-B units only: the frame-unit form of element-aligned views keeps U = 4)
+#ifndef MAVG_AHEAD_NO_U8  // tuning builds: the round-3 4096-frame tiles only (A/B)
+  constexpr bool kU8 = !HS && U0 == 4 && WG == kWG && F * C * (int)sizeof(T) == 16 &&
+                       ((sizeof(T) == 4 && C == 1) || (sizeof(T) == 2 && C == 2));
+#else
+  constexpr bool kU8 = false;
+#endif
+  if constexpr (kU8) {
+    constexpr int TF8 = WG * F * 8;
+    const bool u8 = sizeof(T) == 4 ? !self && ahead_past_l2(k, C, sizeof(T), TF8) && (long long)k <= kAheadU8MaxTiles * TF8
+                                   : !(ahead_past_l2(k, C, sizeof(T), TF) && (long long)k > 384LL * TF);
+    if (u8) return launch_ahead_scan<T, A, C, F, 8, kNtA, kRC, true, false, 0, false, false, WG>(sg, k, st, ws,
+                                                                                              sizeof(T) == 4 ? 320 : 256);
+  }
   // per-wave records: mono only (instantiated for C = 1 alone)
   const bool wrec = C == 1 && (long long)k / TF + 1 <= 64;
   if (wrec) {

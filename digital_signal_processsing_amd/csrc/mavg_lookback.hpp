@@ -382,7 +382,7 @@ __device__ __forceinline__ void run_total(const T* __restrict__ in, const gran_t
 #define MAVG_AHEAD_MINB_I16 1
 #endif
 template <typename T, typename A, int C, int F, int U, int NT, bool RC = false, bool DMA = true, bool WREC = false,
-          int DV = 0, bool HS = false, bool RUNS = false, int WG_ = kWG, bool LATEA = false, bool PW = false>
+          int DV = 0, bool HS = false, bool RUNS = false, int WG_ = kWG, bool LATEA = false, int PW = 0>
 __global__ __launch_bounds__(WG_ + (PW ? 64 : 0),
                              RUNS ? MAVG_AHEAD_RUNS_MINB : (sizeof(T) == 4 ? MAVG_AHEAD_MINB_F32 : MAVG_AHEAD_MINB_I16))
 void ahead_scan_kernel(AheadParams p) {
@@ -502,11 +502,15 @@ void ahead_scan_kernel(AheadParams p) {
 #pragma unroll
         for (int i = 0; i < U * NW; ++i)
           xa[i] = IO::gload(in + (ja * TF + (long long)((i % U) * WG + (i / U) * 64 + lane) * F) * C, eio);
-      // the block's two barriers, passed with the loads in flight (this wave
-      // shares nothing through LDS)
+      // the block's barriers, passed with the loads in flight (this wave
+      // shares nothing through LDS): PW 1 both before the sums, PW 2 the first
+      // only (the publication does not wait for the block's carry)
       __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_s_barrier();
-      if (!produce_any) return;
+      if constexpr (PW == 1) __builtin_amdgcn_s_barrier();
+      if (!produce_any) {
+        if constexpr (PW == 2) __builtin_amdgcn_s_barrier();
+        return;
+      }
       // the loaded values enter the sums only from here: an empty asm that
       // "rewrites" each loaded dword keeps the compiler from hoisting the
       // conversions (and the wait for the loads) above the barriers
@@ -560,6 +564,7 @@ void ahead_scan_kernel(AheadParams p) {
           }
         }
       }
+      if constexpr (PW == 2) __builtin_amdgcn_s_barrier();
       return;
     }
   }

@@ -152,9 +152,9 @@ def test_longest_plan_is_not_truncated():
     longest; its trailing ws= field (tools/tune/ahead_trace.py reads it) must
     be whole."""
     import digital_signal_processsing_amd as dsp
-    p = dsp.plan(1 << 30, 4_000_000)
+    p = dsp.plan(1 << 30, 10_000_000)  # fp32 mono past 1024 8192-frame tiles: the run-total kernel
     assert "runs=1" in p and re.search(r" ws=\d+$", p), p
-    assert 0 < int(p.split(" ws=")[1]) <= dsp.workspace_bytes(1 << 30, 4_000_000), p
+    assert 0 < int(p.split(" ws=")[1]) <= dsp.workspace_bytes(1 << 30, 10_000_000), p
 
 
 def test_workspace_only_for_ahead_scan():
@@ -173,6 +173,10 @@ def test_workspace_only_for_ahead_scan():
     assert dsp.plan(1 << 30, 8192).startswith("ahead_scan<f32,acc=f64,C=1,F=4,U=4")
     assert "wrec=1" in dsp.plan(1 << 30, 20_000) and "ws=%d" % (tiles * 4 * 2 * 8 + 16) in dsp.plan(1 << 30, 20_000)
     assert "wrec=0" in dsp.plan(1 << 30, 300_000) and "ws=%d" % (tiles * 2 * 8 + 16) in dsp.plan(1 << 30, 300_000)
+    # past the L2 reach (window-matched runs): 8192-frame tiles (U=8), one record per tile
+    for k in (600_000, 4_000_000):
+        p = dsp.plan(1 << 30, k)
+        assert "U=8" in p and "wrec=0" in p and "ws=%d" % (tiles // 2 * 2 * 8 + 16) in p, p
     assert dsp.plan(1 << 30, 8192, algo="blelloch_scalar").startswith("ahead_scan<f32,acc=f64,C=1,F=1,U=4")
     assert dsp.workspace_bytes(1 << 30, 8192) == 4 * tiles * 4 * 2 * 8 + 16
     assert dsp.workspace_bytes(1 << 30, 8192, algo="blelloch_scalar") == 4 * tiles * 4 * 2 * 8 + 16

@@ -71,17 +71,31 @@ assert np.array_equal(run(xs, 12_000, 2, "blelloch"), oracle.mavg_i16(xs, 12_000
 assert np.array_equal(run(xs, 70_000, 2, "hillis"), oracle.mavg_i16(xs, 70_000, 2))
 # window-matched runs with run totals (k > 384 tiles; run_total's checks and,
 # with spin 0, the consumers' recompute of every record and run total)
+# (int16 stereo: fp32 mono takes 8192-frame tiles without run totals up to 1024 tiles)
 frames = 4096 * 620 + 5
-plan = dsp.plan(frames, 1_600_000, 1, dsp.F32)
+plan = dsp.plan(frames * 2, 1_600_000, 2, dsp.I16)
 assert plan.startswith("ahead_scan<") and "runs=1" in plan and " remap=1 " not in plan, plan
-xf = oracle.synth_f32(frames, seed=6, dist=2)
-y0 = run(xf, 1_600_000, 1, "auto")
-r = oracle.check_synth_exact(y0, 1_600_000, 1, seed=6, dist=2)
-assert r["mismatches"] == 0, r
+xs = oracle.synth_i16(frames * 2, seed=6)
+y0 = run(xs, 1_600_000, 2, "auto")
+assert np.array_equal(y0, oracle.mavg_i16(xs, 1_600_000, 2))
 lib = _lib.load()
 lib.mavg_test_ahead_schedule(-1, 0)
 try:
-    y1 = run(xf, 1_600_000, 1, "auto")
+    y1 = run(xs, 1_600_000, 2, "auto")
+finally:
+    lib.mavg_test_ahead_schedule(-1, -1)
+assert np.array_equal(y0, y1)
+# fp32 mono 8192-frame tiles with window-matched runs (k = 10^6), recomputed records too
+frames = 8192 * 200 + 5
+plan = dsp.plan(frames, 1_000_000, 1, dsp.F32)
+assert "U=8" in plan and " remap=1 " not in plan and "runs=1" not in plan, plan
+xf = oracle.synth_f32(frames, seed=9, dist=2)
+y0 = run(xf, 1_000_000, 1, "auto")
+r = oracle.check_synth_exact(y0, 1_000_000, 1, seed=9, dist=2)
+assert r["mismatches"] == 0, r
+lib.mavg_test_ahead_schedule(-1, 0)
+try:
+    y1 = run(xf, 1_000_000, 1, "auto")
 finally:
     lib.mavg_test_ahead_schedule(-1, -1)
 assert np.array_equal(y0.view(np.uint8), y1.view(np.uint8))

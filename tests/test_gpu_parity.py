@@ -272,7 +272,8 @@ def test_grouped_xcd_remap_with_tail(oracle_mod, gpu, dtype, C, k):
 @pytest.mark.parametrize("dtype,C,k,algo", [("f32", 1, 600_000, "auto"), ("i16", 2, 1_000_000, "auto"),
                                             ("f32", 1, 4_000_000, "auto"), ("f32", 4, 300_000, "auto"),
                                             ("f32", 1, 700_000, "hillis"), ("f32", 1, 2_000_000, "auto"),
-                                            ("i16", 2, 1_700_000, "auto"), ("i16", 1, 1_500_000, "auto")])
+                                            ("i16", 2, 1_700_000, "auto"), ("i16", 1, 1_500_000, "auto"),
+                                            ("f32", 1, 9_000_000, "auto"), ("i16", 1, 3_500_000, "auto")])
 def test_period_remap_very_long_windows_with_tail(oracle_mod, gpu, dtype, C, k, algo):
     """Windows past the L2 reach: the look-ahead scan runs in window-matched
     runs of G tiles per XCD (remap mode G, 8JG ~ k/T, G not a power of two:
@@ -287,7 +288,10 @@ def test_period_remap_very_long_windows_with_tail(oracle_mod, gpu, dtype, C, k, 
     G = int(plan.split("remap=")[1].split()[0])
     tile = int(plan.split("tile_frames=")[1].split()[0])
     assert _is_long(plan) and G > 1, plan
-    assert ("runs=1" in plan) == (C <= 2 and algo == "auto" and k > 384 * tile and plan.startswith("ahead_scan<")), plan
+    # run totals: the 4096-frame (int16 mono: 8192-frame) U=4 kernel past 384 tiles; fp32 mono and
+    # int16 stereo take 8192-frame tiles (U=8) without them short of that kernel's range
+    assert ("runs=1" in plan) == (C <= 2 and algo == "auto" and k > 384 * tile and plan.startswith("ahead_scan<")
+                                  and "U=8" not in plan), plan
     frames = tile * max(3 * 8 * G + 37, k // tile + 8 * G + 37) + 5  # past one window, 3 periods, a ragged tail
     assert int(dsp.plan(frames * C, k, C, code, algo).split("remap=")[1].split()[0]) == G
     if dtype == "f32":
@@ -494,12 +498,17 @@ def test_ahead_records_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, 
     dt = dsp.F32 if dtype == "f32" else dsp.I16
     frames = 2_600_000 // C + 12_345  # > D = 512 tiles at C=1: the look-ahead producers run
     plan = dsp.plan(frames * C, k, C, dt)
+    tf = int(plan.split("tile_frames=")[1].split()[0])
+    D = int(plan.split(" ahead=")[1].split()[0])
+    if frames < (D + 64) * tf:  # 8192-frame tiles: more than D + 64 of them
+        frames = (D + 64) * tf + 12_345
+        plan = dsp.plan(frames * C, k, C, dt)
     assert _is_long(plan), plan
     if plan.startswith("ahead_scan<"):
-        # mono windows whose per-wave records fit one round of loads take the
-        # per-wave records (wrec=1); the others one record per tile
-        tf = int(plan.split("tile_frames=")[1].split()[0])
-        assert ("wrec=1" in plan) == (C == 1 and k // tf + 1 <= 64), plan
+        # int16 mono windows whose per-wave records fit one round of loads take the
+        # per-wave records (wrec=1); the others (fp32 mono 8192-frame tiles past
+        # the self-published range, multi-channel) one record per tile
+        assert ("wrec=1" in plan) == (C == 1 and "U=8" not in plan and k // tf + 1 <= 64), plan
     if dtype == "f32":
         x = oracle_mod.synth_f32(frames * C, seed=77, dist=2)
     else:

@@ -64,9 +64,18 @@ def test_plans_pick_window_matched_runs_past_the_l2_reach():
     plan = lambda k, C, dt: dsp.plan(1 << 30, k, C, dt)
     remap = lambda k, C, dt: int(re.search(r"remap=(\d+)", plan(k, C, dt)).group(1))
     assert remap(44_100, 1, dsp.F32) == 1 and remap(300_000, 1, dsp.F32) == 1
-    for k, C, dt, tf, ahead in ((600_000, 1, dsp.F32, 4096, 1024), (1_000_000, 1, dsp.F32, 4096, 1024),
-                                (4_000_000, 1, dsp.F32, 4096, 1024), (1_000_000, 2, dsp.I16, 4096, 768),
-                                (1_500_000, 1, dsp.I16, 8192, 1024)):
+    # fp32 mono and int16 stereo: 8192-frame tiles (U=8, D=320 / 256 slots) short of the run
+    # totals (fp32: past 1024 tiles; int16 stereo: the 4096-frame run-total kernel past 384)
+    for k, C, dt, tf, ahead, runs in ((600_000, 1, dsp.F32, 8192, 320, False),
+                                      (1_000_000, 1, dsp.F32, 8192, 320, False),
+                                      (4_000_000, 1, dsp.F32, 8192, 320, False),
+                                      (10_000_000, 1, dsp.F32, 4096, 1024, True),
+                                      (1_000_000, 2, dsp.I16, 8192, 256, False),
+                                      (2_000_000, 2, dsp.I16, 4096, 768, True),
+                                      (1_500_000, 1, dsp.I16, 8192, 1024, False),
+                                      (4_000_000, 1, dsp.I16, 8192, 1024, True)):
+        p = plan(k, C, dt)
+        assert "tile_frames=%d " % tf in p and " ahead=%d " % ahead in p, (k, C, p)
         assert remap(k, C, dt) == run_length(k, tf, ahead), (k, C)
-        assert ("runs=1" in plan(k, C, dt)) == (k > 384 * tf), (k, C)
+        assert ("runs=1" in p) == runs, (k, C, p)
     assert remap(1024, 1, dsp.F32) == 64  # the tile kernel's grouped runs

@@ -59,12 +59,23 @@ void addA(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D = 1024
   vs.push_back({name, [=](hipStream_t s) { return launch_wide_ahead<T, A, C, P, UW, WG, kNtA, DV, F, U>(sg, k, s, ws, D); }, {}});
 }
 
+// the look-ahead scan with U units per lane (tile = U * WG * F frames), as dispatched otherwise
+template <typename T, typename A, int C, int F, int U, bool RC, bool WREC, bool RUNS>
+void addU(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
+  constexpr int kNtA = kNtStore | kNtHalo;
+  char name[80];
+  snprintf(name, sizeof name, "ahead U%d wrec=%d runs=%d D%d", U, (int)WREC, (int)RUNS, D);
+  vs.push_back({name, [=](hipStream_t s) {
+                  return launch_ahead_scan<T, A, C, F, U, kNtA, RC, true, WREC, 0, false, RUNS, 256>(sg, k, s, ws, D);
+                }, {}});
+}
+
 template <int C>
 void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws);
 
 // the look-ahead scan with phase A by LDS-DMA after the first barrier, summed
 // after the in-tile scan (LATEA; per-wave records)
-template <typename T, typename A, int C, int F, bool RC, bool LATE, bool PW = false, bool WREC = true>
+template <typename T, typename A, int C, int F, bool RC, bool LATE, int PW = 0, bool WREC = true>
 void addL(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
   constexpr int kNtA = kNtStore | kNtHalo;
   char name[80];
@@ -80,11 +91,12 @@ void add_wide(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   using T = float;
   using A = double;
   if constexpr (C == 1) {  // mono long windows: the wide look-ahead against the tuned look-ahead
-    addL<T, A, C, 4, true, true>(vs, sg, k, ws, 512);
-    addL<T, A, C, 4, true, false>(vs, sg, k, ws, 512);
-    addL<T, A, C, 4, true, false, true>(vs, sg, k, ws, 512);
-    addL<T, A, C, 4, true, false, true>(vs, sg, k, ws, 768);
-    addL<T, A, C, 4, true, false, true, false>(vs, sg, k, ws, 1024);
+    if (k > 384 * 4096) addU<T, A, C, 4, 4, true, false, true>(vs, sg, k, ws, 1024);
+    else if (k > 63 * 4096) addU<T, A, C, 4, 4, true, false, false>(vs, sg, k, ws, 1024);
+    else addU<T, A, C, 4, 4, true, true, false>(vs, sg, k, ws, 512);
+    addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, 448);
+    addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, 384);
+    addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, 320);
   } else {
     add_wide_c<C>(vs, sg, k, ws);
   }
@@ -142,15 +154,16 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   add_unit<T, A, C, VF>(vs, sg, k, ws);
   if (k > 8192) {  // the look-ahead range
     if constexpr (C == 1) {  // mono: per-wave records, D = 512 (the library's dispatch)
-      addL<T, A, C, 8, false, false, false, true>(vs, sg, k, ws, 512);
-      addL<T, A, C, 8, false, false, true, true>(vs, sg, k, ws, 512);
-      addL<T, A, C, 8, false, false, true, true>(vs, sg, k, ws, 768);
-      addL<T, A, C, 8, false, false, true, false>(vs, sg, k, ws, 1024);
+      addU<T, A, C, 8, 4, false, true, false>(vs, sg, k, ws, 512);
+      addU<T, A, C, 8, 4, false, true, false>(vs, sg, k, ws, 384);
+      addU<T, A, C, 8, 8, false, false, false>(vs, sg, k, ws, 256);
+      addU<T, A, C, 8, 8, false, false, false>(vs, sg, k, ws, 192);
     } else if constexpr (C == 2) {
-      addL<T, A, C, 4, false, false, false, false>(vs, sg, k, ws, 768);
-      addL<T, A, C, 4, false, false, true, false>(vs, sg, k, ws, 768);
-      addL<T, A, C, 4, false, false, true, false>(vs, sg, k, ws, 1024);
-      addL<T, A, C, 4, false, false, true, false>(vs, sg, k, ws, 512);
+      addU<T, A, C, 4, 4, false, false, false>(vs, sg, k, ws, 768);
+      addU<T, A, C, 4, 8, false, false, false>(vs, sg, k, ws, 288);
+      addU<T, A, C, 4, 8, false, false, false>(vs, sg, k, ws, 256);
+      addU<T, A, C, 4, 8, false, false, false>(vs, sg, k, ws, 224);
+      addU<T, A, C, 4, 8, false, false, false>(vs, sg, k, ws, 192);
     } else if constexpr (C == 4) {
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 1024);
     } else {
