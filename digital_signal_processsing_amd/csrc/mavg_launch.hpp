@@ -190,6 +190,47 @@ int launch_wide_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
+// the channel-per-lane tile (mavg_wide.hpp chan_tile_kernel): lanes own one
+// channel of Q frames; same stage, halo and workspace-free launch as the wide tile
+template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0>
+int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
+  constexpr int EPG = 16 / (int)sizeof(T);
+  constexpr int NW = WG / 64;
+  constexpr int TF = WG * Q;
+  constexpr int TG = TF * C / EPG;
+  const long long nframes = sg.nframes;
+  const long long hg = ((long long)k * C + EPG - 1) / EPG;  // granules covering the k-frame halo
+  const long long Hg = (hg + 15) / 16 * 16;                // whole 256-B LDS rows
+  const size_t lds = (size_t)(Hg + TG) * 16 + (size_t)2 * NW * C * sizeof(A);
+  if (lds > 80 * 1024) return MAVG_ERR_UNSUPPORTED;
+  const long long ntiles = (nframes + TF - 1) / TF;
+  if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text),
+             "chan_tile<%s,acc=%s,C=%d,Q=%d,nt=%d,dv=%d> grid=%lld block=%d lds=%zu tile_frames=%d remap=%d",
+             type_name<T>(), type_name<A>(), C, Q, NT, DV, ntiles, WG, lds, TF, xcd_remap);
+    return MAVG_OK;
+  }
+  WideParams p{};
+  p.in = sg.in;
+  p.out = sg.out;
+  p.hist = sg.hist;
+  p.nframes = nframes;
+  p.ntiles = ntiles;
+  p.k = k;
+  p.halo_g = (int)Hg;
+  p.xk_off = 0;
+  p.xcd_remap = xcd_remap;
+  p.pre = sg.pre;
+  p.o = make_out_params(k);
+  if (lds > 64 * 1024) {
+    const int s = raise_dyn_lds_limit<&chan_tile_kernel<T, A, C, Q, WG, NT, DV>>(80 * 1024);
+    if (s != MAVG_OK) return s;
+  }
+  hipLaunchKernelGGL((chan_tile_kernel<T, A, C, Q, WG, NT, DV>), dim3((unsigned)ntiles), dim3(WG), lds, st, p);
+  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+}
+
 // look-ahead scan (one pass over HBM): zero the record granules, then one
 // launch whose tile t publishes the records of tile t + ahead and scans
 // tile t with its carry from earlier records (mavg_lookback.hpp).

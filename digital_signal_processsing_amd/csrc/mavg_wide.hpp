@@ -349,6 +349,207 @@ __global__ __launch_bounds__(WG) void wide_tile_kernel(WideParams p) {
   }
 }
 
+// ----------------------------------------------------------------------------
+// chan_tile_kernel: the wide tile with lanes that own ONE channel each (round
+// 4, fp32 C = 8 and 4).  In wide_tile_kernel a lane's chunk holds every
+// channel of its P frames, so each chunk costs C fp64 wave scans (C = 8: eight
+// 6-step scans per 128 B).  Here lane = b * C + c owns channel c of Q
+// consecutive frames (frame block b of NB = 64 / C per wave): its in-lane sum
+// runs over Q frames of one channel, and ONE scan across the NB lanes of its
+// channel (log2 NB steps at stride C lanes: row_shr DPP inside a 16-lane row,
+// ds_bpermute across rows) serves all C channels at once.
+//
+// The stage is the wide tile's (halo + tile by LDS-DMA, 16-B granules) with a
+// swizzle for the lane-per-channel reads: ds_read_b32 of element (frame
+// m + b*Q, channel c) for the 64 lanes hits granules m*GPF + b*Q*GPF + c/4 --
+// the same 16-B slot of the bank row for every b on the linear layout (an NB-
+// way conflict).  Slot(g) = g ^ (((g >> SH) & (NB - 1)) << LG), SH =
+// log2(Q * GPF), LG = log2(GPF) (GPF granules per frame): the key is b plus a
+// constant for every lane of one read (any m: the low SH bits of m * GPF + c/4
+// never carry into bit SH), so the NB blocks land in NB distinct bank groups,
+// the c/4 bits in the rest: 64 distinct banks.  Like the wide tile's swizzle it
+// permutes granules inside aligned 256 B (an involution), so every LDS-DMA
+// instruction still reads 1 KiB of contiguous global memory, and the outputs
+// written back in the same layout leave as 1-KiB contiguous stores.
+// ----------------------------------------------------------------------------
+constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v / 2); }
+
+template <int C, int Q>
+__device__ __forceinline__ int chan_slot(int g) {
+  constexpr int NB = 64 / C, GPF = C / 4;
+  constexpr int SH = ilog2c(Q * GPF), LG = ilog2c(GPF);
+  return g ^ (((g >> SH) & (NB - 1)) << LG);
+}
+
+template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0>
+__global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
+  static_assert(sizeof(T) == 4 && (C == 4 || C == 8), "fp32 frames of 16 or 32 bytes");
+  constexpr int NW = WG / 64;
+  constexpr int NB = 64 / C;    // frame blocks per wave
+  constexpr int GPF = C / 4;    // 16-B granules per frame
+  constexpr int EPG = 4;        // fp32 elements per granule
+  static_assert(ilog2c(GPF) + ilog2c(NB) == 4 && Q * GPF >= 16, "the key spans one bank row, outside its bits");
+  constexpr int WF = NB * Q;    // frames per wave
+  constexpr int TF = NW * WF;   // tile frames
+  constexpr int TG = TF * GPF;  // tile granules
+  using IO = UnitIO<T, EPG>;
+  using Gr = Unit<T, EPG>;
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int Hg = p.halo_g;
+  unsigned char* sb = smem;                              // [Hg + TG] swizzled granules
+  A* tot = reinterpret_cast<A*>(smem + (Hg + TG) * 16);  // [NW][C] wave-segment totals
+  A* hsum = tot + NW * C;                                // [NW][C] halo partial sums
+  const float* sf = reinterpret_cast<const float*>(sb);
+  // stage element e (frame * C + channel), swizzled
+  auto elem = [&](int e) -> float { return sf[chan_slot<C, Q>(e >> 2) * 4 + (e & 3)]; };
+
+  const T* __restrict__ in = static_cast<const T*>(p.in);
+  T* __restrict__ out = static_cast<T*>(p.out);
+  const T* __restrict__ hist = static_cast<const T*>(p.hist);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int wq = __builtin_amdgcn_readfirstlane(w);
+  const int k = p.k;
+  const long long nframes = p.nframes;
+
+  const long long tile = remap_tile(blockIdx.x, gridDim.x, p.xcd_remap);
+  const long long t0 = tile * TF;
+  const int Hf = Hg * EPG / C;  // staged halo frames (>= k)
+  const long long h0 = t0 - Hf;
+  MAVG_DCHECK(tile >= 0 && tile < p.ntiles && t0 < nframes, "chan tile index", tile, p.ntiles);
+  MAVG_DCHECK(Hf >= k && Hg % 16 == 0, "chan halo", Hf, k);
+  const bool tile_full = t0 + TF <= nframes;
+
+  // ---- stage: halo + tile, swizzled ----
+  if (tile_full && h0 >= 0) {
+    const T* src0 = in + h0 * C;  // logical granule 0
+#pragma unroll
+    for (int i = 0; i < TG / WG; ++i) {
+      const int gl = chan_slot<C, Q>(Hg + i * WG + tid);  // the logical granule this lane's slot holds
+      unsigned char* d = sb + (Hg + i * WG + wq * 64) * 16;
+      if constexpr ((NT & kNtSplit) != 0) {
+        // the last Hg granules of the tile are the next tile's halo: default policy (L2)
+        if (gl >= TG) glds16<false>(src0 + (long long)gl * EPG, d);
+        else glds16<true>(src0 + (long long)gl * EPG, d);
+      } else {
+        glds16<(NT & kNtLoad) != 0>(src0 + (long long)gl * EPG, d);
+      }
+    }
+    for (int j0 = 0; j0 < Hg; j0 += WG) {
+      const int s = j0 + tid;
+      if (s < Hg) glds16<(NT & kNtHalo) != 0>(src0 + (long long)chan_slot<C, Q>(s) * EPG, sb + (j0 + wq * 64) * 16);
+    }
+  } else {
+    // edge tiles: element loads through load_elem (history, peeled head, zeros)
+#pragma unroll 1
+    for (int gl = tid; gl < Hg + TG; gl += WG) {
+      Gr u;
+#pragma unroll
+      for (int i = 0; i < EPG; ++i) {
+        const int e = gl * EPG + i;
+        u.e[i] = load_elem(in, hist, h0 + e / C, e % C, C, nframes, k, p.pre);
+      }
+      IO::store(reinterpret_cast<T*>(sb + chan_slot<C, Q>(gl) * 16), u);
+    }
+  }
+  __syncthreads();
+
+  // ---- halo reduction: W[t0-1] = stage elements [(Hf-k)C, Hf C), per channel ----
+  {
+    const int e0 = (Hf - k) * C;
+    const int g0 = e0 / EPG;
+    A hs[EPG];
+#pragma unroll
+    for (int i = 0; i < EPG; ++i) hs[i] = (A)0;
+    for (int gl = g0 + tid; gl < Hg; gl += WG) {
+      const Gr u = IO::load(reinterpret_cast<const T*>(sb + chan_slot<C, Q>(gl) * 16));
+#pragma unroll
+      for (int i = 0; i < EPG; ++i)
+        if (gl * EPG + i >= e0) hs[i] += to_acc<A>(u.e[i]);
+    }
+    // element i of this thread's granules is channel (cb + i) mod C (granules WG apart: whole frames)
+    const int cb = ((g0 + tid) * EPG) % C;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      A part = (A)0;
+#pragma unroll
+      for (int i = 0; i < EPG; ++i)
+        if (cb + i == c) part += hs[i];
+      const A r = readlane(wave_incl_scan(part), 63);
+      if (lane == 0) hsum[w * C + c] = r;
+    }
+  }
+
+  // ---- pass 1: the lane's channel over its Q frames; the scan across its NB lanes ----
+  const int c = lane & (C - 1);
+  const int b = lane / C;
+  const int f0 = Hf + w * WF + b * Q;  // stage frame of the lane's first frame
+  A run = (A)0;
+#pragma unroll
+  for (int i = 0; i < Q; ++i) run += to_acc<A>(elem((f0 + i) * C + c)) - to_acc<A>(elem((f0 + i - k) * C + c));
+  A incl = run;
+#pragma unroll
+  for (int s = C; s < 64; s <<= 1) {
+    A t;
+    if (s == 4) t = dpp<0x114, 0xf, 0xf>(incl);       // row_shr:4 (zero past the row start)
+    else if (s == 8) t = dpp<0x118, 0xf, 0xf>(incl);  // row_shr:8
+    else {                                            // across 16-lane rows (every lane takes part)
+      t = shfl_up(incl, s);
+      t = lane >= s ? t : (A)0;
+    }
+    incl += t;
+  }
+  if (b == NB - 1) tot[w * C + c] = incl;  // the wave segment's total of channel c
+  __syncthreads();
+
+  // ---- carry: halo sum + the earlier waves' segments of this channel, in wave order ----
+  A base = (A)0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) base += hsum[i * C + c];
+#pragma unroll
+  for (int i = 0; i < NW - 1; ++i)
+    if (i < wq) base += tot[i * C + c];
+  base += incl - run;
+
+  // ---- pass 2: the prefix rebuilt from the stage, outputs ----
+  T yv[Q];
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    base += to_acc<A>(elem((f0 + i) * C + c)) - to_acc<A>(elem((f0 + i - k) * C + c));
+    yv[i] = to_out<T, A, DV>(base, p.o);
+  }
+  if (!tile_full) {  // the ragged last tile: element stores
+    const long long f = t0 + (long long)(w * WF + b * Q);
+#pragma unroll
+    for (int i = 0; i < Q; ++i)
+      if (f + i < nframes) out[(f + i) * C + c] = yv[i];
+    return;
+  }
+  // ---- outputs through LDS (the stage layout), 1 KiB of contiguous output per store ----
+  __syncthreads();  // every read of the stage is done
+  float* sw = reinterpret_cast<float*>(sb);
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    const int e = (f0 + i) * C + c;
+    sw[chan_slot<C, Q>(e >> 2) * 4 + (e & 3)] = yv[i];
+  }
+  // the wave reads back only its own frames: wave-level ordering suffices
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  constexpr int WGR = WF * GPF;  // the wave's granules
+  const int rg = Hg + wq * WGR;
+  T* ob = out + (t0 + (long long)wq * WF) * C;
+#pragma unroll
+  for (int r = 0; r < WGR / 64; ++r) {
+    const int s = rg + r * 64 + lane;  // slot
+    const Gr g = IO::load(reinterpret_cast<const T*>(sb + s * 16));
+    IO::template store<(NT & kNtStore) != 0>(ob + (long long)(chan_slot<C, Q>(s) - rg) * EPG, g);
+  }
+}
+
 }  // namespace mavg
 
 namespace mavg {

@@ -89,3 +89,62 @@ def test_output_writes_conflict_free_and_stores_contiguous(G):
 def test_linear_layout_would_conflict():
     """Why the swizzle exists: the same 64-B chunk reads on the linear layout."""
     assert cycles([(lane * 4) * 16 for lane in range(64)], RB128, 64) == 16
+
+
+# ---------------------------------------------------------------------------
+# chan_tile_kernel (csrc/mavg_wide.hpp): lane = b * C + c reads channel c of
+# frame m + b * Q with ds_read_b32 (and writes its outputs with ds_write_b32):
+# two 32-lane groups, bank = (a/4) mod 32 (MI355X_MICROARCH.md, LDS table).
+# Restated: chan_slot(g) = g ^ (((g >> SH) & (NB - 1)) << LG), SH = log2(Q*GPF),
+# LG = log2(GPF), NB = 64 / C, GPF = C / 4.
+def chan_slot(g, C, Q):
+    nb, gpf = 64 // C, C // 4
+    sh, lg = (Q * gpf).bit_length() - 1, gpf.bit_length() - 1
+    return g ^ (((g >> sh) & (nb - 1)) << lg)
+
+
+CHAN_SHAPES = [(8, 16), (8, 8), (8, 32), (4, 16), (4, 32)]
+
+
+@pytest.mark.parametrize("C,Q", CHAN_SHAPES)
+def test_chan_slot_is_an_involution_inside_256_byte_rows(C, Q):
+    for g in range(1 << 14):
+        s = chan_slot(g, C, Q)
+        assert chan_slot(s, C, Q) == g and s >> 4 == g >> 4
+
+
+def b32_cycles(dword_addrs):
+    total = 0
+    for grp in (range(0, 32), range(32, 64)):
+        banks = {}
+        for lane in grp:
+            banks.setdefault(dword_addrs[lane] % 32, set()).add(dword_addrs[lane])
+        total += max(len(v) for v in banks.values())
+    return total
+
+
+@pytest.mark.parametrize("C,Q", CHAN_SHAPES)
+def test_chan_reads_and_writes_are_conflict_free_at_every_shift(C, Q):
+    """Every (frame m, channel c) read of the 64 lanes -- x at the wave's
+    frames, x[n-k] at any whole-frame shift, the output writes in the same
+    layout -- takes the minimum 2 cycles of a ds_read_b32 / ds_write_b32."""
+    gpf, nb = C // 4, 64 // C
+    for m in range(0, 4 * Q * nb + 37):  # every residue of the first frame
+        addrs = []
+        for lane in range(64):
+            b, c = lane // C, lane % C
+            e = (m + b * Q) * C + c
+            addrs.append(chan_slot(e >> 2, C, Q) * 4 + (e & 3))
+        assert b32_cycles(addrs) == 2, (C, Q, m)
+
+
+@pytest.mark.parametrize("C,Q", CHAN_SHAPES)
+def test_chan_readback_stores_contiguous_kib(C, Q):
+    """The wave's slot-contiguous read-back: lane l of read r takes slot
+    rg + 64 r + l and stores it at its logical granule; each store instruction
+    covers 1 KiB of contiguous output."""
+    wgr = (64 // C) * Q * (C // 4)
+    for rg in (0, 16 * 7, 4096):
+        for r in range(wgr // 64):
+            logical = sorted(chan_slot(rg + 64 * r + l, C, Q) - rg for l in range(64))
+            assert logical == list(range(64 * r, 64 * r + 64))

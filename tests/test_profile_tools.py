@@ -24,6 +24,8 @@ def test_kernel_key_parses_rocprof_names():
     name = "void mavg::ahead_scan_kernel<float, double, 1, 4, 4, 9, true, true, true, 0>(mavg::AheadParams)"
     assert pmc_traffic.kernel_key(name) == ("ahead_scan_kernel",
                                             ("float", "double", "1", "4", "4", "9", "true", "true", "true", "0"))
+    name = "void mavg::chan_tile_kernel<float, double, 8, 16, 512, 13, 0>(mavg::WideParams)"
+    assert pmc_traffic.kernel_key(name) == ("chan_tile_kernel", ("float", "double", "8", "16", "512", "13", "0"))
     assert pmc_traffic.kernel_key("__amd_rocclr_fillBufferAligned") is None
 
 

@@ -43,6 +43,14 @@ void add1(std::vector<Var>& vs, const Sig& sg, int k) {
   vs.push_back({name, [=](hipStream_t s) { return launch_wide_tile<T, A, C, P, U, WG, kNtS, DV>(sg, k, s); }, {}});
 }
 
+template <typename T, typename A, int C, int Q, int WG>
+void addC(std::vector<Var>& vs, const Sig& sg, int k) {
+  constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
+  char name[64];
+  snprintf(name, sizeof name, "chan Q%d %d ntS", Q, WG);
+  vs.push_back({name, [=](hipStream_t s) { return launch_chan_tile<T, A, C, Q, WG, kNtS>(sg, k, s); }, {}});
+}
+
 // the round-3 unit kernels for the same C (tile_scan / ahead_scan, 32-B or 64-B units)
 template <typename T, typename A, int C, int F>
 void add_unit(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
@@ -106,7 +114,7 @@ template <int C>
 void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   using T = float;
   using A = double;
-  if (k > 1024 || (C == 8 && k == 1024)) {  // the look-ahead range: the unit look-ahead against the wide look-ahead shapes
+  if (k > 1024) {  // the look-ahead range: the unit look-ahead against the wide look-ahead shapes
     add_unit<T, A, C, C == 2 ? 2 : 1>(vs, sg, k, ws);
     if constexpr (C == 2) {
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws);
@@ -131,17 +139,16 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     add1<T, A, C, 16, 1>(vs, sg, k);
     add1<T, A, C, 16, 1, 128>(vs, sg, k);
   } else if constexpr (C == 4) {
-    add_unit<T, A, C, 2>(vs, sg, k, ws);
-    add1<T, A, C, 4, 2>(vs, sg, k);
     add1<T, A, C, 8, 1>(vs, sg, k);
-    add1<T, A, C, 8, 2>(vs, sg, k);
-    add1<T, A, C, 8, 1, 128>(vs, sg, k);
+    addC<T, A, C, 16, 256>(vs, sg, k);
+    addC<T, A, C, 16, 512>(vs, sg, k);
+    addC<T, A, C, 32, 256>(vs, sg, k);
   } else {
-    add_unit<T, A, C, 2>(vs, sg, k, ws);
-    add_unit<T, A, C, 1>(vs, sg, k, ws);
     add1<T, A, C, 4, 1>(vs, sg, k);
-    add1<T, A, C, 4, 1, 128>(vs, sg, k);
-    add1<T, A, C, 4, 2, 128>(vs, sg, k);
+    addC<T, A, C, 16, 512>(vs, sg, k);
+    addC<T, A, C, 16, 256>(vs, sg, k);
+    addC<T, A, C, 8, 512>(vs, sg, k);
+    addC<T, A, C, 32, 256>(vs, sg, k);
   }
 }
 
