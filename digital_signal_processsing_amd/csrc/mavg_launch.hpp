@@ -196,7 +196,7 @@ template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0>
 int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
   constexpr int EPG = 16 / (int)sizeof(T);
   constexpr int NW = WG / 64;
-  constexpr int TF = WG * Q;
+  constexpr int TF = NW * (64 / C) * Q;  // waves x frame blocks x frames per block
   constexpr int TG = TF * C / EPG;
   const long long nframes = sg.nframes;
   const long long hg = ((long long)k * C + EPG - 1) / EPG;  // granules covering the k-frame halo
@@ -708,8 +708,12 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
     return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 512);
   } else if constexpr (sizeof(T) == 4 && C == 8) {
-    if (halo_bytes <= 256) return launch_wide_tile<T, A, C, 4, 1, 128, kNtS>(sg, k, st);
-    if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 4, 1, kWG, kNtS>(sg, k, st);
+    // one channel per lane (chan_tile_kernel, 32 frames each): one scan per
+    // tile row for all 8 channels instead of 8 per chunk (in-process A/B,
+    // profiles/r04_tuning/chan/: k=1024 0.543 -> 0.566, 512 0.683 -> 0.688,
+    // 256 0.705 -> 0.723, 7 0.744 -> 0.778 with 128 threads)
+    if (halo_bytes <= 256) return launch_chan_tile<T, A, C, 32, 128, kNtS>(sg, k, st);
+    if (halo_bytes <= 32768) return launch_chan_tile<T, A, C, 32, kWG, kNtS>(sg, k, st);
     if (halo_bytes <= 131072) return launch_wide_ahead<T, A, C, 4, 1, 128, kNtA, 0, 1, 4>(sg, k, st, ws, 512);
     return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
   } else if constexpr (sizeof(T) == 2 && C == 4) {

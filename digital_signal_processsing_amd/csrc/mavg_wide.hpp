@@ -356,8 +356,8 @@ __global__ __launch_bounds__(WG) void wide_tile_kernel(WideParams p) {
 // 6-step scans per 128 B).  Here lane = b * C + c owns channel c of Q
 // consecutive frames (frame block b of NB = 64 / C per wave): its in-lane sum
 // runs over Q frames of one channel, and ONE scan across the NB lanes of its
-// channel (log2 NB steps at stride C lanes: row_shr DPP inside a 16-lane row,
-// ds_bpermute across rows) serves all C channels at once.
+// channel (log2 NB ds_bpermute steps at stride C, 2C, .. lanes) serves all C
+// channels at once.
 //
 // The stage is the wide tile's (halo + tile by LDS-DMA, 16-B granules) with a
 // swizzle for the lane-per-channel reads: ds_read_b32 of element (frame
@@ -489,16 +489,15 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   A run = (A)0;
 #pragma unroll
   for (int i = 0; i < Q; ++i) run += to_acc<A>(elem((f0 + i) * C + c)) - to_acc<A>(elem((f0 + i - k) * C + c));
+  // Kogge-Stone over the NB blocks: steps of 1, 2, 4 .. blocks = C, 2C, 4C ..
+  // lanes.  Every step crosses 16-lane rows for half the lanes (block b - 1 of
+  // an even block lies in the previous row), so row_shr DPP cannot serve it:
+  // ds_bpermute (shfl_up), every lane taking part
   A incl = run;
 #pragma unroll
   for (int s = C; s < 64; s <<= 1) {
-    A t;
-    if (s == 4) t = dpp<0x114, 0xf, 0xf>(incl);       // row_shr:4 (zero past the row start)
-    else if (s == 8) t = dpp<0x118, 0xf, 0xf>(incl);  // row_shr:8
-    else {                                            // across 16-lane rows (every lane takes part)
-      t = shfl_up(incl, s);
-      t = lane >= s ? t : (A)0;
-    }
+    A t = shfl_up(incl, s);
+    t = lane >= s ? t : (A)0;
     incl += t;
   }
   if (b == NB - 1) tot[w * C + c] = incl;  // the wave segment's total of channel c

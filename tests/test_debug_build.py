@@ -106,7 +106,7 @@ r = oracle.check_synth_exact(run(xf, 8192, 1, "auto"), 8192, 1, seed=7, dist=2)
 assert r["mismatches"] == 0, r
 # 8 fp32 channels: the wide tile (k <= 1024) and the look-ahead scan's 64-B units past it;
 # stereo fp32 with an odd window (the half-granule x[n-k] extraction)
-for C, k, kern in ((8, 1024, "wide_tile<"), (8, 3000, "wide_ahead<"), (2, 1023, "wide_tile<"), (4, 7, "wide_tile<"),
+for C, k, kern in ((8, 1024, "chan_tile<"), (8, 5, "chan_tile<"), (8, 3000, "wide_ahead<"), (2, 1023, "wide_tile<"), (4, 7, "wide_tile<"),
                    (4, 9000, "wide_ahead<"), (2, 20_000, "wide_ahead<")):
     assert dsp.plan(300_007 * C, k, C, dsp.F32).startswith(kern), (C, k)
     xf = oracle.synth_f32(300_007 * C, seed=8, dist=1)

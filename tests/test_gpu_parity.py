@@ -601,7 +601,7 @@ def _wide_windows(dsp, C, dt=None):
 def test_wide_tile_every_window_edge(oracle_mod, gpu, C):
     """fp32 multi-channel frames run the wide-frame tile scan (mavg_wide.hpp:
     chunks of P consecutive frames per lane, swizzled LDS stage, outputs through
-    LDS): every window where the plan changes (halo rows, tile shapes, the switch
+    LDS; 8 channels: chan_tile_kernel, one channel of 32 frames per lane): every window where the plan changes (halo rows, tile shapes, the switch
     to the look-ahead scan) and one frame either side, odd windows (the
     half-granule x[n-k] shift at C=2), on rounding data (dist 2) against the
     exact window sums, with a ragged tail tile."""
@@ -614,7 +614,8 @@ def test_wide_tile_every_window_edge(oracle_mod, gpu, C):
         x = oracle_mod.synth_f32(frames * C, seed=k, dist=2)
         r = oracle_mod.check_synth_exact(_run(x, k, C, "blelloch", gpu), k, C, seed=k, dist=2, rtol=RTOL)
         assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, (k, plan, r)
-    assert any(p.startswith("wide_tile<") for p in seen) and any(p.startswith("wide_ahead<") for p in seen), seen
+    tile = "chan_tile<" if C == 8 else "wide_tile<"  # 8 channels: one channel per lane
+    assert any(p.startswith(tile) for p in seen) and any(p.startswith("wide_ahead<") for p in seen), seen
 
 
 @pytest.mark.parametrize("C", [4, 8])
@@ -648,7 +649,8 @@ def test_wide_tile_short_signals_history_and_views(oracle_mod, gpu, C, k):
     32-B-aligned views), against the oracle."""
     import digital_signal_processsing_amd as dsp
     import torch
-    assert dsp.plan(1 << 24, k, C, dsp.F32).startswith("wide_tile<"), dsp.plan(1 << 24, k, C, dsp.F32)
+    assert dsp.plan(1 << 24, k, C, dsp.F32).startswith("chan_tile<" if C == 8 else "wide_tile<"), dsp.plan(
+        1 << 24, k, C, dsp.F32)
     for frames in (1, 5, k, 2 * k + 3, 100_003):
         x = oracle_mod.synth_f32(frames * C, offset=frames + k, dist=1)
         assert_f32_close(_run(x, k, C, "blelloch", gpu), oracle_mod.mavg_f32(x, k, C), f"frames={frames}")

@@ -145,10 +145,11 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     addC<T, A, C, 32, 256>(vs, sg, k);
   } else {
     add1<T, A, C, 4, 1>(vs, sg, k);
-    addC<T, A, C, 16, 512>(vs, sg, k);
-    addC<T, A, C, 16, 256>(vs, sg, k);
-    addC<T, A, C, 8, 512>(vs, sg, k);
     addC<T, A, C, 32, 256>(vs, sg, k);
+    addC<T, A, C, 64, 128>(vs, sg, k);
+    addC<T, A, C, 64, 256>(vs, sg, k);
+    addC<T, A, C, 32, 128>(vs, sg, k);
+    addC<T, A, C, 32, 512>(vs, sg, k);
   }
 }
 
