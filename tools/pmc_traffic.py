@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 TYPE = {"f32": "float", "f64": "double", "i16": "short", "i32": "int", "i64": "long"}
 FAMILY = {"tile_scan": "tile_scan_kernel", "direct": "direct_kernel",
           "naive": "naive_kernel", "ahead_scan": "ahead_scan_kernel",
-          "wide_tile": "wide_tile_kernel", "wide_ahead": "wide_ahead_kernel"}
+          "wide_tile": "wide_tile_kernel", "wide_ahead": "wide_ahead_kernel", "chan_tile": "chan_tile_kernel"}
 
 
 def kernel_key(name):
