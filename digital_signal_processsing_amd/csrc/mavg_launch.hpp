@@ -476,13 +476,12 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
 // wide look-ahead scan (mavg_wide.hpp): the look-ahead record carry in its
 // unit layout (F frames x U units per lane, per-tile records) with the wide
 // in-tile scan (P-frame chunks x UW rows); 16-B-aligned views only.
-template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U>
+template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false>
 int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
   constexpr int NW = WG / 64;
   constexpr int EPG = 16 / (int)sizeof(T);
-  constexpr int G = P * C / EPG;
-  constexpr int TF = WG * P * UW;
-  constexpr int TG = WG * UW * G;
+  constexpr int TF = CH ? NW * (64 / C) * P : WG * P * UW;  // CH: P frames of one channel per lane
+  constexpr int TG = TF * C / EPG;
   constexpr int NSEG = UW * NW;
   using SA = typename ScanAcc<T, A>::type;
   const long long nframes = sg.nframes;
@@ -508,9 +507,10 @@ int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   if (lds > 80 * 1024) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "wide_ahead<%s,acc=%s,C=%d,P=%d,U=%d,nt=%d,dv=%d,F=%d,FU=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
+             "wide_ahead<%s,acc=%s,C=%d,P=%d,U=%d,nt=%d,dv=%d,F=%d,FU=%d%s> grid=%lld block=%d lds=%zu tile_frames=%d "
              "ahead=%d remap=%d ws=%zu",
-             type_name<T>(), type_name<A>(), C, P, UW, NT, DV, F, U, ntiles, WG, lds, TF, ahead, xcd_remap, need);
+             type_name<T>(), type_name<A>(), C, P, UW, NT, DV, F, U, CH ? ",ch=1" : "", ntiles, WG, lds, TF, ahead,
+             xcd_remap, need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -539,10 +539,11 @@ int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.runs = nullptr;
   p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
   if (lds > 64 * 1024) {
-    const int s = raise_dyn_lds_limit<&wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U>>(80 * 1024);
+    const int s = raise_dyn_lds_limit<&wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH>>(80 * 1024);
     if (s != MAVG_OK) return s;
   }
-  hipLaunchKernelGGL((wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U>), dim3((unsigned)ntiles), dim3(WG), lds, st, p);
+  hipLaunchKernelGGL((wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH>), dim3((unsigned)ntiles), dim3(WG), lds, st,
+                     p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 

@@ -569,17 +569,24 @@ namespace mavg {
 // Per-wave records, run totals, self-publication and the Hillis-Steele form
 // stay in ahead_scan_kernel (mono / int16 paths).
 // ----------------------------------------------------------------------------
-template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U>
+// CH (round 4, fp32 C = 8): the in-tile scan of chan_tile_kernel instead of
+// the chunks -- lane = b * C + c owns channel c of P (= Q) consecutive frames,
+// one ds_bpermute scan across a channel's lanes, the chan_slot stage layout
+// (UW = 1); the record carry is unchanged.
+template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false>
 __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
   constexpr int NW = WG / 64;
   constexpr int EPG = 16 / (int)sizeof(T);
-  constexpr int CE = P * C;
+  constexpr int CE = CH ? 4 * C : P * C;   // (CH: unused)
   constexpr int G = CE / EPG;
   static_assert(CE % EPG == 0 && (G == 4 || G == 8), "64-B or 128-B chunks");
+  static_assert(!CH || (sizeof(T) == 4 && UW == 1 && (C == 4 || C == 8)), "channel-per-lane form: fp32, C = 4 or 8");
   constexpr int QM = G == 4 ? 3 : 7;
-  constexpr int TF = WG * P * UW;
+  constexpr int NB = 64 / C;               // CH: frame blocks per wave
+  constexpr int WF = NB * P;               // CH: frames per wave
+  constexpr int TF = CH ? NW * WF : WG * P * UW;
   static_assert(TF == WG * F * U, "the record units tile the same frames as the chunks");
-  constexpr int TG = WG * UW * G;  // tile granules
+  constexpr int TG = TF * C / EPG;  // tile granules
   constexpr int SG = TG + 1;       // shifted-tile granules (one more for an x[n-k] extraction)
   constexpr int NSEG = UW * NW;
   constexpr int VE = F * C;
@@ -621,6 +628,10 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
   const int pcount = a >= 0 ? (int)(jlo * TF - a) : 0;
   const long long nitem = qhi - qlo;
 
+  auto slot = [](int g) -> int {
+    if constexpr (CH) return chan_slot<C, P>(g);
+    else return stage_slot<QM>(g);
+  };
   // ---- 1. the tile and the shifted tile to LDS; phase A; own / head-duty records ----
   const unsigned nb = gridDim.x;
   const unsigned bd = blockIdx.x + (unsigned)p.ahead;
@@ -629,8 +640,8 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
   if (tile_full) {
     const T* src = in + t0 * C;
 #pragma unroll
-    for (int i = 0; i < UW * G; ++i) {
-      const int gl = stage_slot<QM>(i * WG + tid);
+    for (int i = 0; i < TG / WG; ++i) {
+      const int gl = slot(i * WG + tid);
       glds16<(NT & kNtLoad) != 0>(src + (long long)gl * EPG, tstage + (i * WG + wq * 64) * 16);
     }
   } else {
@@ -642,7 +653,7 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
         const int e = gl * EPG + i;
         u.e[i] = load_elem(in, hist, t0 + e / C, e % C, C, nframes, k, pre);
       }
-      GIO::store(reinterpret_cast<T*>(tstage + stage_slot<QM>(gl) * 16), u);
+      GIO::store(reinterpret_cast<T*>(tstage + slot(gl) * 16), u);
     }
   }
   const bool stage_fast = h0 >= 0 && (h0 * C + (long long)SG * EPG) <= nframes * C;
@@ -650,7 +661,7 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
     const T* src = in + h0 * C;
     for (int j0 = 0; j0 < SG; j0 += WG) {
       const int s = j0 + tid;
-      if (s < SG) glds16<(NT & kNtHalo) != 0>(src + (long long)stage_slot<QM>(s) * EPG, sstage + (j0 + wq * 64) * 16);
+      if (s < SG) glds16<(NT & kNtHalo) != 0>(src + (long long)slot(s) * EPG, sstage + (j0 + wq * 64) * 16);
     }
   } else {
 #pragma unroll 1
@@ -661,7 +672,7 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
         const int e = gl * EPG + i;
         u.e[i] = load_elem(in, hist, h0 + e / C, e % C, C, nframes, k, pre);
       }
-      GIO::store(reinterpret_cast<T*>(sstage + stage_slot<QM>(gl) * 16), u);
+      GIO::store(reinterpret_cast<T*>(sstage + slot(gl) * 16), u);
     }
   }
   auto share = [&](int src, const SA (&r)[C]) {
@@ -766,9 +777,36 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
       }
     }
   };
+  // CH: the lane's channel over its P frames, then the scan across the NB
+  // lanes of the channel (chan_tile_kernel); the partial window's x[n-k] of
+  // the lane's channel in hpo
+  const int cl = lane & (C - 1);  // CH: the lane's channel (= cc: WG is a multiple of C)
+  const int j0 = w * WF + (lane / C) * P;
+  const float* tsf = reinterpret_cast<const float*>(tstage);
+  const float* ssf = reinterpret_cast<const float*>(sstage);
+  auto tel = [&](int e) -> float { return tsf[chan_slot<C, P>(e >> 2) * 4 + (e & 3)]; };
+  auto sel = [&](int e) -> float { return ssf[chan_slot<C, P>(e >> 2) * 4 + (e & 3)]; };
+  SA crun = (SA)0, cincl = (SA)0;
+  A hpo = (A)0;
+  if constexpr (CH) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const float xk = sel((Ha - k + j0 + i) * C + cl);
+      if (j0 + i < pcount) hpo += to_acc<A>(xk);
+      crun += to_acc<SA>(tel((j0 + i) * C + cl)) - to_acc<SA>(xk);
+    }
+    cincl = crun;
+#pragma unroll
+    for (int sh = C; sh < 64; sh <<= 1) {
+      SA t = shfl_up(cincl, sh);
+      t = lane >= sh ? t : (SA)0;
+      cincl += t;
+    }
+    if (lane >= 64 - C) tot[w * C + cl] = cincl;
+  }
   SA lx[UW][C];
 #pragma unroll
-  for (int uw = 0; uw < UW; ++uw) {
+  for (int uw = 0; uw < UW && !CH; ++uw) {
     const int j = uw * WG + tid;
     uint32_t xv[NWD], xk[NWD];
     x_chunk(j, xv);
@@ -852,12 +890,54 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
   }
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    const A r = readlane(wave_incl_scan(hp[c] + (cc == c ? hq : (A)0)), 63);
+    const A r = readlane(wave_incl_scan(hp[c] + (cc == c ? hq + hpo : (A)0)), 63);
     if (lane == 0) hsum[w * C + c] = r;
   }
   __syncthreads();
 
   // ---- 5. carry + earlier segments; pass 2 rebuilt from the stages; outputs ----
+  if constexpr (CH) {
+    A base = (A)0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) base += hsum[i * C + cl];
+#pragma unroll
+    for (int i = 0; i < NW - 1; ++i)
+      if (i < wq) base += (A)tot[i * C + cl];
+    base += (A)(cincl - crun);
+    T yv[P];
+    SA run = (SA)0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      run += to_acc<SA>(tel((j0 + i) * C + cl)) - to_acc<SA>(sel((Ha - k + j0 + i) * C + cl));
+      yv[i] = to_out<T, A, DV>(base + (A)run, p.o);
+    }
+    if (!tile_full) {
+#pragma unroll
+      for (int i = 0; i < P; ++i)
+        if (t0 + j0 + i < nframes) out[(t0 + j0 + i) * C + cl] = yv[i];
+      return;
+    }
+    __syncthreads();  // every read of the tile stage is done: it takes the outputs
+    float* tw = reinterpret_cast<float*>(tstage);
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int e = (j0 + i) * C + cl;
+      tw[chan_slot<C, P>(e >> 2) * 4 + (e & 3)] = yv[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int WGR = WF * C / EPG;  // the wave's granules
+    const int rg = wq * WGR;
+    T* ob = out + (t0 + (long long)wq * WF) * C;
+#pragma unroll
+    for (int r = 0; r < WGR / 64; ++r) {
+      const int s2 = rg + r * 64 + lane;
+      const Gr g = GIO::load(reinterpret_cast<const T*>(tstage + s2 * 16));
+      GIO::template store<(NT & kNtStore) != 0>(ob + (long long)(chan_slot<C, P>(s2) - rg) * EPG, g);
+    }
+    return;
+  }
   static_assert(NSEG <= 64, "segment totals are scanned across one wave");
   A w0[C];
   SA ex[C];

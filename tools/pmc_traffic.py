@@ -65,7 +65,8 @@ def plan_key(plan):
     elif fam == "chan_tile":
         args = (T, acc, kv["C"], kv["Q"], wg, kv["nt"], kv.get("dv", "0"))
     elif fam == "wide_ahead":
-        args = (T, acc, kv["C"], kv["P"], kv["U"], wg, kv["nt"], kv.get("dv", "0"), kv["F"], kv["FU"])
+        args = (T, acc, kv["C"], kv["P"], kv["U"], wg, kv["nt"], kv.get("dv", "0"), kv["F"], kv["FU"],
+                "true" if kv.get("ch", "0") == "1" else "false")
     else:
         args = (T, acc)
     return FAMILY[fam], args

@@ -78,6 +78,15 @@ void addU(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
                 }, {}});
 }
 
+// the wide look-ahead scan with the channel-per-lane in-tile scan (CH)
+template <typename T, typename A, int C, int Q, int WG, int F, int U>
+void addAC(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
+  constexpr int kNtA = kNtStore | kNtHalo;
+  char name[80];
+  snprintf(name, sizeof name, "wahead chan Q%d %d F%d U%d D%d", Q, WG, F, U, D);
+  vs.push_back({name, [=](hipStream_t s) { return launch_wide_ahead<T, A, C, Q, 1, WG, kNtA, 0, F, U, true>(sg, k, s, ws, D); }, {}});
+}
+
 template <int C>
 void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws);
 
@@ -121,14 +130,16 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
       addA<T, A, C, 16, 1, 256, 2, 8>(vs, sg, k, ws);
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 512);
     } else if constexpr (C == 4) {
-      addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws);
-      addA<T, A, C, 8, 1, 256, 1, 8>(vs, sg, k, ws);
       addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 16, 256, 1, 4>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 32, 256, 1, 8>(vs, sg, k, ws, 512);
     } else {
       addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws);
-      addA<T, A, C, 4, 1, 128, 1, 4>(vs, sg, k, ws);
-      addA<T, A, C, 2, 1, 256, 1, 2>(vs, sg, k, ws);
       addA<T, A, C, 4, 1, 128, 1, 4>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 32, 256, 1, 4>(vs, sg, k, ws, 1024);
+      addAC<T, A, C, 32, 256, 1, 4>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 32, 128, 1, 4>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 16, 256, 1, 2>(vs, sg, k, ws, 1024);
     }
     if (k > 4096) return;
   }
