@@ -331,5 +331,9 @@ constexpr int kNtLoad = 2;
 // them in L2), and nt loads for the halo itself (its last use)
 constexpr int kNtSplit = 4;
 constexpr int kNtHalo = 8;
+// look-ahead scan only: phase A's loads of tile t + D non-temporal (very long
+// windows: the prefetched tile then leaves the XCD's L2 before the window's
+// lines do; its own workgroup's later loads are served by L2 or the MALL)
+constexpr int kNtPhaseA = 16;
 
 }  // namespace mavg

@@ -447,7 +447,16 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     constexpr int TF8 = WG * F * 8;
     const bool u8 = sizeof(T) == 4 ? !self && ahead_past_l2(k, C, sizeof(T), TF8) && (long long)k <= kAheadU8MaxTiles * TF8
                                    : !(ahead_past_l2(k, C, sizeof(T), TF) && (long long)k > 384LL * TF);
-    if (u8) return launch_ahead_scan<T, A, C, F, 8, kNtA, kRC, true, false, 0, false, false, WG>(sg, k, st, ws,
+    // phase A keeps the default policy: non-temporal phase-A loads (kNtPhaseA, tuning builds
+    // -DMAVG_AHEAD_NTA) measured +3-4 % in the in-process tuner but -15 to -18 % in bench.py's
+    // timing (profiles/r04_tuning/u8/nta_*, bench_timing_nta_*: k=4e6 0.620 -> 0.510, 2e6
+    // 0.652 -> 0.546, 1e6 0.660 -> 0.556, 6e5 0.664 -> 0.557)
+#ifdef MAVG_AHEAD_NTA
+    constexpr int kNt8 = sizeof(T) == 4 ? (kNtA | kNtPhaseA) : kNtA;
+#else
+    constexpr int kNt8 = kNtA;
+#endif
+    if (u8) return launch_ahead_scan<T, A, C, F, 8, kNt8, kRC, true, false, 0, false, false, WG>(sg, k, st, ws,
                                                                                               sizeof(T) == 4 ? 320 : 256);
   }
   // per-wave records: mono only (instantiated for C = 1 alone)
@@ -712,11 +721,20 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     // one channel per lane (chan_tile_kernel, 32 frames each): one scan per
     // tile row for all 8 channels instead of 8 per chunk (in-process A/B,
     // profiles/r04_tuning/chan/: k=1024 0.543 -> 0.566, 512 0.683 -> 0.688,
-    // 256 0.705 -> 0.723, 7 0.744 -> 0.778 with 128 threads)
+    // 256 0.705 -> 0.723, 7 0.744 -> 0.778 with 128 threads); past its halo the
+    // same in-tile scan in the look-ahead carry (CH): k=2048 0.464 -> 0.488,
+    // 4096 0.462 -> 0.487 (128 threads), 44100 0.390 -> 0.433 (256, D = 512)
+#ifndef MAVG_NO_CHAN
     if (halo_bytes <= 256) return launch_chan_tile<T, A, C, 32, 128, kNtS>(sg, k, st);
     if (halo_bytes <= 32768) return launch_chan_tile<T, A, C, 32, kWG, kNtS>(sg, k, st);
+    if (halo_bytes <= 131072) return launch_wide_ahead<T, A, C, 32, 1, 128, kNtA, 0, 1, 4, true>(sg, k, st, ws, 512);
+    return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 4, true>(sg, k, st, ws, 512);
+#else  // tuning builds: the chunk-per-lane kernels (A/B)
+    if (halo_bytes <= 256) return launch_wide_tile<T, A, C, 4, 1, 128, kNtS>(sg, k, st);
+    if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 4, 1, kWG, kNtS>(sg, k, st);
     if (halo_bytes <= 131072) return launch_wide_ahead<T, A, C, 4, 1, 128, kNtA, 0, 1, 4>(sg, k, st, ws, 512);
     return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
+#endif
   } else if constexpr (sizeof(T) == 2 && C == 4) {
     if constexpr (sizeof(A) == 4) {
       if (halo_bytes <= 8192) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);

@@ -372,6 +372,11 @@ __device__ __forceinline__ void run_total(const T* __restrict__ in, const gran_t
 #define MAVG_ANOW() 0ull
 #endif
 
+#ifdef MAVG_AHEAD_PHASEA_NT  // tuning builds: per-tile phase A loads non-temporal (A/B)
+constexpr bool kPhaseANt = true;
+#else
+constexpr bool kPhaseANt = false;
+#endif
 #ifndef MAVG_AHEAD_RUNS_MINB  // tuning builds: workgroups per CU the RUNS kernel is compiled for
 #define MAVG_AHEAD_RUNS_MINB 1
 #endif
@@ -641,7 +646,8 @@ void ahead_scan_kernel(AheadParams p) {
   if (produce && !LATEA) {
     if constexpr (!WREC)
 #pragma unroll
-      for (int u = 0; u < U; ++u) xa[u] = IO::gload(in + (ja * TF + (long long)(u * WG + tid) * F) * C, eio);
+      for (int u = 0; u < U; ++u)
+        xa[u] = IO::template gload<kPhaseANt || (NT & kNtPhaseA) != 0>(in + (ja * TF + (long long)(u * WG + tid) * F) * C, eio);
     SA r[C];
     wave_record<T, SA, C, F, U>(xa, r);
     share(0, ja, r);
