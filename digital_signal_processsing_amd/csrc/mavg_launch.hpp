@@ -289,7 +289,7 @@ inline bool ahead_past_l2(long long k, int C, int elem, int TF) {
   return k * C * elem > (1LL << 21) && k >= 8LL * TF;
 }
 template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0, bool HS = false,
-          bool RUNS = false, int WG = kWG, bool LATEA = false, int PW = 0>
+          bool RUNS = false, int WG = kWG>
 int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead, bool self = false) {
   constexpr int NW = WG / 64;
   const long long nframes = sg.nframes;
@@ -346,7 +346,7 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
 #endif
   const size_t need = rec_bytes + run_bytes + 16 + trace_bytes;
   size_t lds = kStageBytes + (size_t)NW * C * sizeof(A) + (size_t)(NSEG + 3 * NW) * C * sizeof(SA);
-  if (HS || LATEA) lds = (lds + 15) / 16 * 16 + (size_t)U * WG * VE * sizeof(T);  // + the tile (HS) / phase A's tile
+  if (HS) lds = (lds + 15) / 16 * 16 + (size_t)U * WG * VE * sizeof(T);  // + the tile
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
 #ifdef MAVG_AHEAD_LDS_MIN  // tuning builds: fewer workgroups per CU through a bigger LDS allocation
   lds = std::max<size_t>(lds, MAVG_AHEAD_LDS_MIN);
@@ -354,10 +354,9 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
              "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dma=%d,wrec=%d,dv=%d> grid=%lld block=%d lds=%zu "
-             "tile_frames=%d ahead=%d remap=%d%s%s%s%s ws=%zu",
+             "tile_frames=%d ahead=%d remap=%d%s%s ws=%zu",
              type_name<T>(), type_name<A>(), C, F, U, HS ? "hillis" : "blelloch", NT, (int)RC, (int)DMA, (int)WREC, DV,
-             ntiles, WG, lds, TF, ahead, xcd_remap, RUNS ? " runs=1" : "", self ? " self=1" : "", LATEA ? " latea=1" : "",
-             PW == 1 ? " pw=1" : PW == 2 ? " pw=2" : "", need);
+             ntiles, WG, lds, TF, ahead, xcd_remap, RUNS ? " runs=1" : "", self ? " self=1" : "", need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -388,8 +387,8 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
 #ifdef MAVG_AHEAD_TRACE
   p.trace = reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(ws.ptr) + need - trace_bytes);
 #endif
-  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV, HS, RUNS, WG, LATEA, PW>),
-                     dim3((unsigned)ntiles), dim3(WG + (PW ? 64 : 0)), lds, st, p);
+  hipLaunchKernelGGL((ahead_scan_kernel<T, A, C, F, U, NT, RC, DMA, WREC, DV, HS, RUNS, WG>), dim3((unsigned)ntiles),
+                     dim3(WG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 

@@ -372,11 +372,6 @@ __device__ __forceinline__ void run_total(const T* __restrict__ in, const gran_t
 #define MAVG_ANOW() 0ull
 #endif
 
-#ifdef MAVG_AHEAD_PHASEA_NT  // tuning builds: per-tile phase A loads non-temporal (A/B)
-constexpr bool kPhaseANt = true;
-#else
-constexpr bool kPhaseANt = false;
-#endif
 #ifndef MAVG_AHEAD_RUNS_MINB  // tuning builds: workgroups per CU the RUNS kernel is compiled for
 #define MAVG_AHEAD_RUNS_MINB 1
 #endif
@@ -387,25 +382,11 @@ constexpr bool kPhaseANt = false;
 #define MAVG_AHEAD_MINB_I16 1
 #endif
 template <typename T, typename A, int C, int F, int U, int NT, bool RC = false, bool DMA = true, bool WREC = false,
-          int DV = 0, bool HS = false, bool RUNS = false, int WG_ = kWG, bool LATEA = false, int PW = 0>
-__global__ __launch_bounds__(WG_ + (PW ? 64 : 0),
-                             RUNS ? MAVG_AHEAD_RUNS_MINB : (sizeof(T) == 4 ? MAVG_AHEAD_MINB_F32 : MAVG_AHEAD_MINB_I16))
+          int DV = 0, bool HS = false, bool RUNS = false, int WG_ = kWG>
+__global__ __launch_bounds__(WG_, RUNS ? MAVG_AHEAD_RUNS_MINB : (sizeof(T) == 4 ? MAVG_AHEAD_MINB_F32 : MAVG_AHEAD_MINB_I16))
 void ahead_scan_kernel(AheadParams p) {
   static_assert(!(HS && RC), "the Hillis-Steele flavour keeps its per-element prefixes");
   static_assert(!(RUNS && WREC), "run totals sum per-tile records");
-  // LATEA: phase A by LDS-DMA into a stage of its own, issued after the first
-  // barrier and summed after the in-tile scan, so its HBM latency overlaps the
-  // scan instead of preceding it, with no registers held across the scan;
-  // per-wave records only (each wave sums the part of the stage its own DMA
-  // filled: no barrier before publication)
-  static_assert(!LATEA || (WREC && !HS && !RUNS), "late phase A: per-wave records, Blelloch flavour");
-  // PW: phase A in a producer wave of its own (the block's wave NW, after the
-  // NW scan waves): it issues the loads of tile t + D first thing, passes both
-  // block barriers without waiting for them, and sums and publishes the
-  // record(s) after the second barrier, so the scan waves never wait on the
-  // HBM fetch (their own loads are the L2 hits an earlier producer left).
-  // The records are the same sequences as wave_record / publish_record_lds.
-  static_assert(!(PW && LATEA), "one place for phase A");
   constexpr int WG = WG_;
   constexpr int NW = WG / 64;
   constexpr int VE = F * C;
@@ -426,8 +407,7 @@ void ahead_scan_kernel(AheadParams p) {
   A* hsum = reinterpret_cast<A*>(smem + kStageBytes);  // [NW][C] carry partials
   SA* tot = reinterpret_cast<SA*>(hsum + NW * C);       // [NSEG][C] segment totals
   SA* shares = tot + NSEG * C;                           // [3][NW][C] wave shares of the records published here
-  // HS: the tile itself, [U*WG] units, after the shares (16-B aligned); LATEA:
-  // phase A's tile there instead
+  // HS: the tile itself, [U*WG] units, after the shares (16-B aligned)
   T* tstage = reinterpret_cast<T*>(smem + ((kStageBytes + (NW * C * (int)sizeof(A)) +
                                             (NSEG + 3 * NW) * C * (int)sizeof(SA) + 15) & ~15));
 
@@ -499,83 +479,9 @@ void ahead_scan_kernel(AheadParams p) {
   const unsigned nb = gridDim.x;
   const unsigned bd = blockIdx.x + (unsigned)p.ahead;  // the block D dispatch slots later (same XCD)
   const long long ja = bd < nb ? map_tile(bd) : -1;
-  const bool produce_any = !p.self && ja >= 0 && ja < p.nfull;
-  if constexpr (PW) {
-    if (wq == NW) {  // the producer wave
-      U_t xa[U * NW];  // slot i = wv * U + u: unit u * WG + wv * 64 + lane
-      if (produce_any)
-#pragma unroll
-        for (int i = 0; i < U * NW; ++i)
-          xa[i] = IO::gload(in + (ja * TF + (long long)((i % U) * WG + (i / U) * 64 + lane) * F) * C, eio);
-      // the block's barriers, passed with the loads in flight (this wave
-      // shares nothing through LDS): PW 1 both before the sums, PW 2 the first
-      // only (the publication does not wait for the block's carry)
-      __builtin_amdgcn_s_barrier();
-      if constexpr (PW == 1) __builtin_amdgcn_s_barrier();
-      if (!produce_any) {
-        if constexpr (PW == 2) __builtin_amdgcn_s_barrier();
-        return;
-      }
-      // the loaded values enter the sums only from here: an empty asm that
-      // "rewrites" each loaded dword keeps the compiler from hoisting the
-      // conversions (and the wait for the loads) above the barriers
-#pragma unroll
-      for (int i = 0; i < U * NW; ++i) {
-        static_assert(sizeof(U_t) % 4 == 0, "units of whole dwords");
-        uint32_t dw[sizeof(U_t) / 4];
-        __builtin_memcpy(dw, &xa[i], sizeof(U_t));
-#pragma unroll
-        for (int d = 0; d < (int)(sizeof(U_t) / 4); ++d) asm volatile("" : "+v"(dw[d]));
-        __builtin_memcpy(&xa[i], dw, sizeof(U_t));
-      }
-      SA rec[C];
-#pragma unroll
-      for (int wv = 0; wv < NW; ++wv) {
-        SA ls[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) ls[c] = (SA)0;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int fr = 0; fr < F; ++fr)
-#pragma unroll
-            for (int c = 0; c < C; ++c) ls[c] += to_acc<SA>(xa[wv * U + u].e[fr * C + c]);
-        SA r[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) r[c] = readlane(wave_incl_scan(ls[c]), 63);
-        if constexpr (WREC) {
-          publish_record<SA, C>(gran, ja * NW + wv, r, lane);
-        } else {
-#pragma unroll
-          for (int c = 0; c < C; ++c) rec[c] = wv == 0 ? r[c] : rec[c] + r[c];
-        }
-      }
-      if constexpr (!WREC) publish_record<SA, C>(gran, ja, rec, lane);
-      if constexpr (RUNS) {  // the run total that comes with this record (as wave 3 below)
-        const long long G = p.xcd_remap;
-        if ((ja + 1) % G == 0) {
-          const long long rr = (ja + 1) / G - 1 - 8;
-          if (rr >= 0 && rr < p.runs_done) {
-            A tt[C];
-            run_total<T, A, C, F, U, WG>(in, gran, rr * G, (int)G, p.spin, lane, eio, tt, p.stats);
-            if (lane < C * NGA) {
-              const int c = lane / NGA, h = lane - c * NGA;
-              A v = tt[0];
-#pragma unroll
-              for (int i = 1; i < C; ++i)
-                if (c == i) v = tt[i];
-              gran_store((gran_t*)p.runs + (rr * C + c) * NGA + h, gran_word(v, h));
-            }
-          }
-        }
-      }
-      if constexpr (PW == 2) __builtin_amdgcn_s_barrier();
-      return;
-    }
-  }
-  const bool produce = produce_any && !PW;  // phase A by the scan waves
+  const bool produce = !p.self && ja >= 0 && ja < p.nfull;
   U_t xa[U];
-  if constexpr (WREC && !LATEA) {  // phase A's loads first: the HBM fetch with the longest latency
+  if constexpr (WREC) {  // phase A's loads first: the HBM fetch with the longest latency
     if (produce)
 #pragma unroll
       for (int u = 0; u < U; ++u) xa[u] = IO::gload(in + (ja * TF + (long long)(u * WG + tid) * F) * C, eio);
@@ -643,11 +549,11 @@ void ahead_scan_kernel(AheadParams p) {
       for (int c = 0; c < C; ++c) shares[(src * NW + w) * C + c] = r[c];
     }
   };
-  if (produce && !LATEA) {
+  if (produce) {
     if constexpr (!WREC)
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        xa[u] = IO::template gload<kPhaseANt || (NT & kNtPhaseA) != 0>(in + (ja * TF + (long long)(u * WG + tid) * F) * C, eio);
+        xa[u] = IO::template gload<(NT & kNtPhaseA) != 0>(in + (ja * TF + (long long)(u * WG + tid) * F) * C, eio);
     SA r[C];
     wave_record<T, SA, C, F, U>(xa, r);
     share(0, ja, r);
@@ -726,18 +632,6 @@ void ahead_scan_kernel(AheadParams p) {
           }
         }
       }
-    }
-  }
-
-  // LATEA: phase A's tile to its own stage now (default policy: the tile's own
-  // later loads hit L2); nothing waits for it before the in-tile scan is done
-  const bool late_a = LATEA && produce && !eio;
-  if constexpr (LATEA && kDma) {
-    if (late_a) {
-      unsigned char* ab = reinterpret_cast<unsigned char*>(tstage);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        glds16<false>(in + (ja * TF + (long long)(u * WG + tid) * F) * C, ab + (u * WG + wq * 64) * 16);
     }
   }
 
@@ -844,36 +738,6 @@ void ahead_scan_kernel(AheadParams p) {
       lx[u][c] = incl - run[c];
       const SA segtot = readlane(incl, 63);
       if (lane == 0) tot[(u * NW + w) * C + c] = segtot;
-    }
-  }
-
-  // LATEA: the wave's share of phase A's record from its own part of the stage
-  // (units u*WG + w*64 + lane: wave_record's order, the same bits), published
-  if constexpr (LATEA) {
-    if (produce) {
-      SA r[C];
-      if (late_a) {
-        // the LDS-DMA writes count on vmcnt and the compiler does not order
-        // this wave's reads of its own DMA destination after them: wait here
-        // (every other vector-memory load of the tile is consumed by now)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        SA ls[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) ls[c] = (SA)0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const U_t xu = IO::load(tstage + (u * WG + tid) * VE);
-#pragma unroll
-          for (int fr = 0; fr < F; ++fr)
-#pragma unroll
-            for (int c = 0; c < C; ++c) ls[c] += to_acc<SA>(xu.e[fr * C + c]);
-        }
-#pragma unroll
-        for (int c = 0; c < C; ++c) r[c] = readlane(wave_incl_scan(ls[c]), 63);
-      } else {  // element-aligned views: the record from global memory
-        wave_record_lean<T, SA, C, F, U, WG>(in, ja, w, lane, eio, r);
-      }
-      share(0, ja, r);
     }
   }
 

@@ -58,8 +58,7 @@ def plan_key(plan):
     elif fam == "ahead_scan":
         b = {"0": "false", "1": "true"}
         args = (T, acc, kv["C"], kv["F"], kv["U"], kv["nt"], b[kv["rc"]], b[kv["dma"]], b[kv["wrec"]], kv["dv"], hs,
-                "true" if " runs=1" in plan else "false", wg, "true" if " latea=1" in plan else "false",
-                "1" if " pw=1" in plan else "2" if " pw=2" in plan else "0")
+                "true" if " runs=1" in plan else "false", wg)
     elif fam == "wide_tile":
         args = (T, acc, kv["C"], kv["P"], kv["U"], wg, kv["nt"], kv.get("dv", "0"))
     elif fam == "chan_tile":

@@ -90,19 +90,6 @@ void addAC(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
 template <int C>
 void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws);
 
-// the look-ahead scan with phase A by LDS-DMA after the first barrier, summed
-// after the in-tile scan (LATEA; per-wave records)
-template <typename T, typename A, int C, int F, bool RC, bool LATE, int PW = 0, bool WREC = true>
-void addL(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
-  constexpr int kNtA = kNtStore | kNtHalo;
-  char name[80];
-  snprintf(name, sizeof name, "ahead wrec=%d D%d latea=%d pw=%d", (int)WREC, D, (int)LATE, (int)PW);
-  vs.push_back({name, [=](hipStream_t s) {
-                  return launch_ahead_scan<T, A, C, F, 4, kNtA, RC, true, WREC, 0, false, false, 256, LATE, PW>(sg, k, s,
-                                                                                                                ws, D);
-                }, {}});
-}
-
 template <int C>
 void add_wide(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   using T = float;
