@@ -165,11 +165,13 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
       addU<T, A, C, 8, 8, false, false, false>(vs, sg, k, ws, 256);
       addU<T, A, C, 8, 8, false, false, false>(vs, sg, k, ws, 192);
     } else if constexpr (C == 2) {
-      addU<T, A, C, 4, 4, false, false, false>(vs, sg, k, ws, 768);
-      addU<T, A, C, 4, 8, false, false, false>(vs, sg, k, ws, 288);
       addU<T, A, C, 4, 8, false, false, false>(vs, sg, k, ws, 256);
-      addU<T, A, C, 4, 8, false, false, false>(vs, sg, k, ws, 224);
-      addU<T, A, C, 4, 8, false, false, false>(vs, sg, k, ws, 192);
+      addU<T, A, C, 4, 4, true, false, false>(vs, sg, k, ws, 768);   // recompute-from-registers (RC)
+      addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, 256);
+      addU<T, A, C, 4, 4, false, true, false>(vs, sg, k, ws, 512);   // per-wave records for stereo
+      addU<T, A, C, 4, 4, false, true, false>(vs, sg, k, ws, 384);
+      addU<T, A, C, 4, 8, false, true, false>(vs, sg, k, ws, 192);
+      addU<T, A, C, 4, 8, false, true, false>(vs, sg, k, ws, 128);
     } else if constexpr (C == 4) {
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 1024);
     } else {
