@@ -16,4 +16,8 @@ for spec in "44100 2 i16" "44100 1 i16" "44100 1 f32" "4000000 1 f32"; do
 done
 timeout -k 10 150 tools/tune/wide_ab 30 44100 2 6 1 i16 > "$OUT/records_i16_c2_k44100.log" 2>&1 || exit $?
 cat "$OUT/records_i16_c2_k44100.log"
+for k in 44100 20000; do  # int16 4 channels past the wide tile: the wide look-ahead against the unit look-ahead
+  timeout -k 10 150 tools/tune/wide_ab 30 $k 4 6 1 i16 > "$OUT/wide_i16_c4_k$k.log" 2>&1 || exit $?
+  cat "$OUT/wide_i16_c4_k$k.log"
+done
 exit 0

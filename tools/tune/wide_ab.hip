@@ -174,6 +174,8 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
       addU<T, A, C, 4, 8, false, true, false>(vs, sg, k, ws, 128);
     } else if constexpr (C == 4) {
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 1024);
+      addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 512);
+      addA<T, A, C, 16, 1, 256, 4, 4>(vs, sg, k, ws, 512);
     } else {
       addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws, 1024);
       addA<T, A, C, 8, 1, 256, 1, 8>(vs, sg, k, ws, 1024);
