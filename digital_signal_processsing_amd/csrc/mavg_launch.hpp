@@ -738,6 +738,13 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     if constexpr (sizeof(A) == 4) {
       if (halo_bytes <= 8192) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
       if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 16, 1, kWG, kNtS>(sg, k, st);
+#ifndef MAVG_NO_I16C4_WIDE_AHEAD
+      // past it the wide look-ahead (64-B chunks, D = 512) instead of the 16-B unit look-ahead
+      // (in-process A/B, profiles/r04_tuning/wide/wide_i16_c4_*: k=44100 0.579 -> 0.598, 20000
+      // 0.590 -> 0.602; bench timing, bit-exact, profiles/r04_tuning/wide/bench_timing_i16_c4_*:
+      // k=44100 0.575 -> 0.586, 60000 0.582 -> 0.591, 20000 0.587 -> 0.590)
+      return launch_wide_ahead<T, A, C, 8, 1, kWG, kNtA, 0, 2, 4>(sg, k, st, ws, 512);
+#endif
     }
   } else if constexpr (sizeof(T) == 2 && C == 8) {
     if constexpr (sizeof(A) == 4) {
