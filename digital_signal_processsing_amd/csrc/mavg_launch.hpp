@@ -192,7 +192,7 @@ int launch_wide_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
 
 // the channel-per-lane tile (mavg_wide.hpp chan_tile_kernel): lanes own one
 // channel of Q frames; same stage, halo and workspace-free launch as the wide tile
-template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0>
+template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false>
 int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
   constexpr int EPG = 16 / (int)sizeof(T);
   constexpr int NW = WG / 64;
@@ -201,14 +201,15 @@ int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
   const long long nframes = sg.nframes;
   const long long hg = ((long long)k * C + EPG - 1) / EPG;  // granules covering the k-frame halo
   const long long Hg = (hg + 15) / 16 * 16;                // whole 256-B LDS rows
-  const size_t lds = (size_t)(Hg + TG) * 16 + (size_t)2 * NW * C * sizeof(A);
+  if (XG && (long long)k < TF) return MAVG_ERR_UNSUPPORTED;  // x[n-k] must lie in the halo
+  const size_t lds = (size_t)(Hg + (XG ? 0 : TG)) * 16 + (size_t)2 * NW * C * sizeof(A);
   if (lds > 80 * 1024) return MAVG_ERR_UNSUPPORTED;
   const long long ntiles = (nframes + TF - 1) / TF;
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "chan_tile<%s,acc=%s,C=%d,Q=%d,nt=%d,dv=%d> grid=%lld block=%d lds=%zu tile_frames=%d remap=%d",
-             type_name<T>(), type_name<A>(), C, Q, NT, DV, ntiles, WG, lds, TF, xcd_remap);
+             "chan_tile<%s,acc=%s,C=%d,Q=%d,nt=%d,dv=%d%s> grid=%lld block=%d lds=%zu tile_frames=%d remap=%d",
+             type_name<T>(), type_name<A>(), C, Q, NT, DV, XG ? ",xg=1" : "", ntiles, WG, lds, TF, xcd_remap);
     return MAVG_OK;
   }
   WideParams p{};
@@ -224,10 +225,10 @@ int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
   p.pre = sg.pre;
   p.o = make_out_params(k);
   if (lds > 64 * 1024) {
-    const int s = raise_dyn_lds_limit<&chan_tile_kernel<T, A, C, Q, WG, NT, DV>>(80 * 1024);
+    const int s = raise_dyn_lds_limit<&chan_tile_kernel<T, A, C, Q, WG, NT, DV, XG>>(80 * 1024);
     if (s != MAVG_OK) return s;
   }
-  hipLaunchKernelGGL((chan_tile_kernel<T, A, C, Q, WG, NT, DV>), dim3((unsigned)ntiles), dim3(WG), lds, st, p);
+  hipLaunchKernelGGL((chan_tile_kernel<T, A, C, Q, WG, NT, DV, XG>), dim3((unsigned)ntiles), dim3(WG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 

@@ -381,7 +381,13 @@ __device__ __forceinline__ int chan_slot(int g) {
   return g ^ (((g >> SH) & (NB - 1)) << LG);
 }
 
-template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0>
+// XG (windows of at least a tile, k >= TF): only the halo is staged; each lane
+// loads its own Q values of x straight from global memory (4-B loads, 8
+// 32-B segments per wave instruction, every line used whole over 4 frames),
+// since every x[n-k] of the tile then lies in the halo.  Half the LDS at
+// k = TF (C = 8, k = 1024: 32 KiB, four workgroups per CU instead of two);
+// the outputs are staged in the halo region after the last read of it.
+template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false>
 __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   static_assert(sizeof(T) == 4 && (C == 4 || C == 8), "fp32 frames of 16 or 32 bytes");
   constexpr int NW = WG / 64;
@@ -398,7 +404,7 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int Hg = p.halo_g;
   unsigned char* sb = smem;                              // [Hg + TG] swizzled granules
-  A* tot = reinterpret_cast<A*>(smem + (Hg + TG) * 16);  // [NW][C] wave-segment totals
+  A* tot = reinterpret_cast<A*>(smem + (Hg + (XG ? 0 : TG)) * 16);  // [NW][C] wave-segment totals
   A* hsum = tot + NW * C;                                // [NW][C] halo partial sums
   const float* sf = reinterpret_cast<const float*>(sb);
   // stage element e (frame * C + channel), swizzled
@@ -420,13 +426,28 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   const long long h0 = t0 - Hf;
   MAVG_DCHECK(tile >= 0 && tile < p.ntiles && t0 < nframes, "chan tile index", tile, p.ntiles);
   MAVG_DCHECK(Hf >= k && Hg % 16 == 0, "chan halo", Hf, k);
+  MAVG_DCHECK(!XG || (k >= TF && Hg >= TG), "chan XG window", k, TF);
   const bool tile_full = t0 + TF <= nframes;
+  constexpr int kTileStaged = XG ? 0 : TG;  // granules of the tile in the stage
+  const int c = lane & (C - 1);
+  const int b = lane / C;
+  const int jl = w * WF + b * Q;  // tile frame of the lane's first frame
+  T xr[XG ? Q : 1];
+  if constexpr (XG) {  // the lane's x, issued before the stage
+    if (tile_full) {
+#pragma unroll
+      for (int i = 0; i < Q; ++i) xr[i] = in[(t0 + jl + i) * C + c];
+    } else {
+#pragma unroll
+      for (int i = 0; i < Q; ++i) xr[i] = load_elem(in, hist, t0 + jl + i, c, C, nframes, k, p.pre);
+    }
+  }
 
   // ---- stage: halo + tile, swizzled ----
   if (tile_full && h0 >= 0) {
     const T* src0 = in + h0 * C;  // logical granule 0
 #pragma unroll
-    for (int i = 0; i < TG / WG; ++i) {
+    for (int i = 0; i < kTileStaged / WG; ++i) {
       const int gl = chan_slot<C, Q>(Hg + i * WG + tid);  // the logical granule this lane's slot holds
       unsigned char* d = sb + (Hg + i * WG + wq * 64) * 16;
       if constexpr ((NT & kNtSplit) != 0) {
@@ -444,7 +465,7 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   } else {
     // edge tiles: element loads through load_elem (history, peeled head, zeros)
 #pragma unroll 1
-    for (int gl = tid; gl < Hg + TG; gl += WG) {
+    for (int gl = tid; gl < Hg + kTileStaged; gl += WG) {
       Gr u;
 #pragma unroll
       for (int i = 0; i < EPG; ++i) {
@@ -483,12 +504,14 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   }
 
   // ---- pass 1: the lane's channel over its Q frames; the scan across its NB lanes ----
-  const int c = lane & (C - 1);
-  const int b = lane / C;
-  const int f0 = Hf + w * WF + b * Q;  // stage frame of the lane's first frame
+  const int f0 = Hf + jl;  // stage frame of the lane's first frame
+  auto xv = [&](int i) -> T {
+    if constexpr (XG) return xr[i];
+    else return elem((f0 + i) * C + c);
+  };
   A run = (A)0;
 #pragma unroll
-  for (int i = 0; i < Q; ++i) run += to_acc<A>(elem((f0 + i) * C + c)) - to_acc<A>(elem((f0 + i - k) * C + c));
+  for (int i = 0; i < Q; ++i) run += to_acc<A>(xv(i)) - to_acc<A>(elem((f0 + i - k) * C + c));
   // Kogge-Stone over the NB blocks: steps of 1, 2, 4 .. blocks = C, 2C, 4C ..
   // lanes.  Every step crosses 16-lane rows for half the lanes (block b - 1 of
   // an even block lies in the previous row), so row_shr DPP cannot serve it:
@@ -516,11 +539,11 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   T yv[Q];
 #pragma unroll
   for (int i = 0; i < Q; ++i) {
-    base += to_acc<A>(elem((f0 + i) * C + c)) - to_acc<A>(elem((f0 + i - k) * C + c));
+    base += to_acc<A>(xv(i)) - to_acc<A>(elem((f0 + i - k) * C + c));
     yv[i] = to_out<T, A, DV>(base, p.o);
   }
   if (!tile_full) {  // the ragged last tile: element stores
-    const long long f = t0 + (long long)(w * WF + b * Q);
+    const long long f = t0 + (long long)jl;
 #pragma unroll
     for (int i = 0; i < Q; ++i)
       if (f + i < nframes) out[(f + i) * C + c] = yv[i];
@@ -529,9 +552,10 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   // ---- outputs through LDS (the stage layout), 1 KiB of contiguous output per store ----
   __syncthreads();  // every read of the stage is done
   float* sw = reinterpret_cast<float*>(sb);
+  const int fo = (XG ? 0 : Hf) + jl;  // XG: the outputs take the halo region (Hg >= TG granules)
 #pragma unroll
   for (int i = 0; i < Q; ++i) {
-    const int e = (f0 + i) * C + c;
+    const int e = (fo + i) * C + c;
     sw[chan_slot<C, Q>(e >> 2) * 4 + (e & 3)] = yv[i];
   }
   // the wave reads back only its own frames: wave-level ordering suffices
@@ -539,7 +563,7 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   constexpr int WGR = WF * GPF;  // the wave's granules
-  const int rg = Hg + wq * WGR;
+  const int rg = (XG ? 0 : Hg) + wq * WGR;
   T* ob = out + (t0 + (long long)wq * WF) * C;
 #pragma unroll
   for (int r = 0; r < WGR / 64; ++r) {

@@ -43,12 +43,11 @@ void add1(std::vector<Var>& vs, const Sig& sg, int k) {
   vs.push_back({name, [=](hipStream_t s) { return launch_wide_tile<T, A, C, P, U, WG, kNtS, DV>(sg, k, s); }, {}});
 }
 
-template <typename T, typename A, int C, int Q, int WG>
+template <typename T, typename A, int C, int Q, int WG, bool XG = false, int NT = kNtSplit | kNtHalo | kNtStore>
 void addC(std::vector<Var>& vs, const Sig& sg, int k) {
-  constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
   char name[64];
-  snprintf(name, sizeof name, "chan Q%d %d ntS", Q, WG);
-  vs.push_back({name, [=](hipStream_t s) { return launch_chan_tile<T, A, C, Q, WG, kNtS>(sg, k, s); }, {}});
+  snprintf(name, sizeof name, "chan Q%d %d nt%d xg%d", Q, WG, NT, (int)XG);
+  vs.push_back({name, [=](hipStream_t s) { return launch_chan_tile<T, A, C, Q, WG, NT, 0, XG>(sg, k, s); }, {}});
 }
 
 // the round-3 unit kernels for the same C (tile_scan / ahead_scan, 32-B or 64-B units)
@@ -142,12 +141,11 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     addC<T, A, C, 16, 512>(vs, sg, k);
     addC<T, A, C, 32, 256>(vs, sg, k);
   } else {
-    add1<T, A, C, 4, 1>(vs, sg, k);
-    addC<T, A, C, 32, 256>(vs, sg, k);
-    addC<T, A, C, 64, 128>(vs, sg, k);
-    addC<T, A, C, 64, 256>(vs, sg, k);
-    addC<T, A, C, 32, 128>(vs, sg, k);
-    addC<T, A, C, 32, 512>(vs, sg, k);
+    addC<T, A, C, 32, 256, true>(vs, sg, k);
+    addC<T, A, C, 32, 256, true, kNtHalo | kNtStore>(vs, sg, k);
+    addC<T, A, C, 16, 256, true>(vs, sg, k);
+    addC<T, A, C, 16, 512, true>(vs, sg, k);
+    addC<T, A, C, 32, 128, true>(vs, sg, k);
   }
 }
 
