@@ -726,6 +726,14 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     // 4096 0.462 -> 0.487 (128 threads), 44100 0.390 -> 0.433 (256, D = 512)
 #ifndef MAVG_NO_CHAN
     if (halo_bytes <= 256) return launch_chan_tile<T, A, C, 32, 128, kNtS>(sg, k, st);
+#ifndef MAVG_NO_CHAN_XG
+    // windows of at least a tile: stage the halo only, x straight from global memory (XG: half
+    // the LDS, twice the workgroups per CU; bench timing, profiles/r04_tuning/chan/bench_timing_xg_*:
+    // k=1024 0.562 -> 0.737 (1024-frame tiles, bit-identical), 768 0.583 -> 0.647, 512 0.671 ->
+    // 0.739 (512-frame tiles); in-process xg_*: 0.563 -> 0.748, 0.582 -> 0.682, 0.675 -> 0.751)
+    if (halo_bytes <= 32768 && k >= 1024) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
+    if (halo_bytes <= 32768 && k >= 512) return launch_chan_tile<T, A, C, 32, 128, kNtS, 0, true>(sg, k, st);
+#endif
     if (halo_bytes <= 32768) return launch_chan_tile<T, A, C, 32, kWG, kNtS>(sg, k, st);
     if (halo_bytes <= 131072) return launch_wide_ahead<T, A, C, 32, 1, 128, kNtA, 0, 1, 4, true>(sg, k, st, ws, 512);
     return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 4, true>(sg, k, st, ws, 512);

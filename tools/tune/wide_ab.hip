@@ -137,15 +137,14 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     add1<T, A, C, 16, 1, 128>(vs, sg, k);
   } else if constexpr (C == 4) {
     add1<T, A, C, 8, 1>(vs, sg, k);
-    addC<T, A, C, 16, 256>(vs, sg, k);
-    addC<T, A, C, 16, 512>(vs, sg, k);
-    addC<T, A, C, 32, 256>(vs, sg, k);
-  } else {
-    addC<T, A, C, 32, 256, true>(vs, sg, k);
-    addC<T, A, C, 32, 256, true, kNtHalo | kNtStore>(vs, sg, k);
     addC<T, A, C, 16, 256, true>(vs, sg, k);
-    addC<T, A, C, 16, 512, true>(vs, sg, k);
+    addC<T, A, C, 32, 256, true>(vs, sg, k);
+    addC<T, A, C, 16, 128, true>(vs, sg, k);
+  } else {
+    addC<T, A, C, 32, 256>(vs, sg, k);
+    addC<T, A, C, 32, 256, true>(vs, sg, k);
     addC<T, A, C, 32, 128, true>(vs, sg, k);
+    addC<T, A, C, 16, 128, true>(vs, sg, k);
   }
 }
 
