@@ -714,6 +714,12 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 16, 1, kWG, kNtS>(sg, k, st);
     return launch_wide_ahead<T, A, C, 8, 1, kWG, kNtA, 0, 2, 4>(sg, k, st, ws, 512);
   } else if constexpr (sizeof(T) == 4 && C == 4) {
+#ifndef MAVG_NO_CHAN_XG
+    // 2048 <= k <= 3584: the halo-only channel-per-lane tile (2048-frame tiles; in-process,
+    // profiles/r04_tuning/chan/xg_c4_*, xgr_*: k=2048 0.660 -> 0.712 against the wide tile, 3000
+    // 0.541 -> 0.675 against the wide look-ahead; k=4096 ties it, 0.559 vs 0.556)
+    if (k >= 2048 && halo_bytes <= 57344) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
+#endif
     if (halo_bytes <= 4096) return launch_wide_tile<T, A, C, 8, 2, kWG, kNtS>(sg, k, st);
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
     return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 512);
@@ -731,7 +737,9 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     // the LDS, twice the workgroups per CU; bench timing, profiles/r04_tuning/chan/bench_timing_xg_*:
     // k=1024 0.562 -> 0.737 (1024-frame tiles, bit-identical), 768 0.583 -> 0.647, 512 0.671 ->
     // 0.739 (512-frame tiles); in-process xg_*: 0.563 -> 0.748, 0.582 -> 0.682, 0.675 -> 0.751)
-    if (halo_bytes <= 32768 && k >= 1024) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
+    // up to 64 KiB of halo (k <= 2048), where the wide look-ahead took over (in-process,
+    // profiles/r04_tuning/chan/xgr_*: k=1536 0.478 -> 0.656, 2048 0.482 -> 0.548)
+    if (halo_bytes <= 65536 && k >= 1024) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
     if (halo_bytes <= 32768 && k >= 512) return launch_chan_tile<T, A, C, 32, 128, kNtS, 0, true>(sg, k, st);
 #endif
     if (halo_bytes <= 32768) return launch_chan_tile<T, A, C, 32, kWG, kNtS>(sg, k, st);

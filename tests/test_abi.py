@@ -128,8 +128,9 @@ def test_plan_describes_launch_without_gpu():
     assert dsp.plan(1 << 30, 1024, channels=4).startswith("wide_tile<f32,acc=f64,C=4,P=8,U=1")
     assert dsp.plan(1 << 30, 1024, channels=8).startswith("chan_tile<f32,acc=f64,C=8,Q=32")  # a channel per lane
     assert ",xg=1>" in dsp.plan(1 << 30, 1024, channels=8) and ",xg=1>" not in dsp.plan(1 << 30, 511, channels=8)
-    assert dsp.plan(1 << 30, 1025, channels=8).startswith("wide_ahead<f32,acc=f64,C=8,P=32") and ",ch=1>" in dsp.plan(
-        1 << 30, 1025, channels=8)
+    assert dsp.plan(1 << 30, 2049, channels=8).startswith("wide_ahead<f32,acc=f64,C=8,P=32") and ",ch=1>" in dsp.plan(
+        1 << 30, 2049, channels=8)
+    assert ",xg=1>" in dsp.plan(1 << 30, 2048, channels=8) and ",xg=1>" in dsp.plan(1 << 30, 3000, channels=4)
     assert dsp.plan(3 << 28, 1024, channels=3).startswith("tile_scan<f32")  # 12-B frames: frame units
     assert dsp.plan(1 << 30, 1024, channels=2, algo="hillis").startswith("tile_scan<")
     # int16 keeps the register-staged tiles (bench.py's timing, tools/tune/ab_libs.py)

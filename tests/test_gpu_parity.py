@@ -649,8 +649,8 @@ def test_wide_tile_short_signals_history_and_views(oracle_mod, gpu, C, k):
     32-B-aligned views), against the oracle."""
     import digital_signal_processsing_amd as dsp
     import torch
-    assert dsp.plan(1 << 24, k, C, dsp.F32).startswith("chan_tile<" if C == 8 else "wide_tile<"), dsp.plan(
-        1 << 24, k, C, dsp.F32)
+    assert dsp.plan(1 << 24, k, C, dsp.F32).split("<")[0] in ("wide_tile", "chan_tile"), dsp.plan(1 << 24, k, C,
+                                                                                                   dsp.F32)
     for frames in (1, 5, k, 2 * k + 3, 100_003):
         x = oracle_mod.synth_f32(frames * C, offset=frames + k, dist=1)
         assert_f32_close(_run(x, k, C, "blelloch", gpu), oracle_mod.mavg_f32(x, k, C), f"frames={frames}")
@@ -676,7 +676,38 @@ def test_wide_tile_short_signals_history_and_views(oracle_mod, gpu, C, k):
         assert_f32_close(yb[2:].cpu().numpy(), full, "view +8 B")
 
 
-@pytest.mark.parametrize("C,k", [(4, 4097), (4, 44_100), (8, 1025), (8, 44_100), (2, 4097)])
+@pytest.mark.parametrize("C,k", [(8, 512), (8, 1000), (8, 1024), (8, 1537), (8, 2048), (4, 2048), (4, 3001),
+                                 (4, 3584)])
+def test_chan_tile_halo_only_stage(oracle_mod, gpu, C, k):
+    """The channel-per-lane tile with only the halo staged (xg=1: x from global
+    memory, outputs staged in the halo region): rounding data against the exact
+    window sums with a ragged tail, signals shorter than a tile, a history and
+    a 32-B (C=8) / 16-B (C=4) offset view, against the oracle."""
+    import digital_signal_processsing_amd as dsp
+    import torch
+    frames = 9 * 1024 + 333
+    plan = dsp.plan(frames * C, k, C, dsp.F32)
+    assert plan.startswith("chan_tile<") and ",xg=1>" in plan, plan
+    x = oracle_mod.synth_f32(frames * C, seed=k + C, dist=2)
+    r = oracle_mod.check_synth_exact(_run(x, k, C, "blelloch", gpu), k, C, seed=k + C, dist=2, rtol=RTOL)
+    assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, (plan, r)
+    for short in (1, 7, k - 1, k + 5):
+        xs = oracle_mod.synth_f32(short * C, offset=short, dist=1)
+        assert_f32_close(_run(xs, k, C, "blelloch", gpu), oracle_mod.mavg_f32(xs, k, C), f"frames={short}")
+    x = oracle_mod.synth_f32(frames * C, offset=3, dist=1)
+    full = oracle_mod.mavg_f32(x, k, C)
+    cut = k + 1111
+    hist = x[(cut - (k - 1)) * C: cut * C].copy()
+    assert_f32_close(_run(x[cut * C:], k, C, "blelloch", gpu, history=hist), full[cut * C:], "history")
+    off = 8 if C == 8 else 4
+    xb = torch.zeros(frames * C + off, dtype=torch.float32, device=gpu)
+    xb[off:] = torch.from_numpy(x).to(gpu)
+    yb = torch.zeros_like(xb)
+    dsp.moving_average_into(xb[off:], yb[off:], k, C, "blelloch")
+    assert_f32_close(yb[off:].cpu().numpy(), full, f"view +{off * 4} B")
+
+
+@pytest.mark.parametrize("C,k", [(4, 4097), (4, 44_100), (8, 2049), (8, 44_100), (2, 4097)])
 def test_f32_multichannel_long_windows_every_form(oracle_mod, gpu, C, k):
     """Past the wide tile's LDS-staged halo (the wide look-ahead scan):
     rounding data against the exact sums, a view 16 B (C=8: 32 B) into an
@@ -701,7 +732,7 @@ def test_f32_multichannel_long_windows_every_form(oracle_mod, gpu, C, k):
     assert_f32_close(_run(x, k, C, "blelloch_scalar", gpu), ref, f"k={k} scalar")
 
 
-@pytest.mark.parametrize("C,k", [(2, 4097), (2, 44_100), (4, 2049), (4, 20_000), (8, 1025), (8, 44_100),
+@pytest.mark.parametrize("C,k", [(2, 4097), (2, 44_100), (4, 3585), (4, 20_000), (8, 2049), (8, 44_100),
                                  (8, 700_000)])
 def test_wide_ahead_bitwise_whatever_the_schedule(oracle_mod, gpu, C, k):
     """Multi-channel fp32 windows past the wide tile run the wide look-ahead
