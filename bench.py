@@ -66,6 +66,17 @@ WORKLOADS = {
     "f32_stereo_2p30": (1 << 30, 1024, 2, "f32", "blelloch"),
     "f32_c4_2p30": (1 << 30, 1024, 4, "f32", "blelloch"),
     "f32_c8_2p30": (1 << 30, 1024, 8, "f32", "blelloch"),
+    # multi-channel windows past the LDS-staged halo (the wide look-ahead scan) and at the edge of
+    # the halo-only channel tile, and the reference's int16 PCM at the channel counts its WAV
+    # reader accepts (wav_header.h:26-48)
+    "f32_stereo_long": (1 << 30, 44100, 2, "f32", "blelloch"),
+    "f32_c4_long": (1 << 30, 44100, 4, "f32", "blelloch"),
+    "f32_c8_long": (1 << 30, 44100, 8, "f32", "blelloch"),
+    "f32_c8_k2048": (1 << 30, 2048, 8, "f32", "blelloch"),
+    "i16_c4_2p30": (1 << 30, 1024, 4, "i16", "blelloch"),
+    "i16_c8_2p30": (1 << 30, 1024, 8, "i16", "blelloch"),
+    "i16_c4_long": (1 << 30, 44100, 4, "i16", "blelloch"),
+    "i16_c8_long": (1 << 30, 44100, 8, "i16", "blelloch"),
 }
 
 

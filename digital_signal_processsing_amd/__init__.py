@@ -82,8 +82,10 @@ def workspace_bytes(n: int, grade: int, channels: int = 1, dtype: int = F32, alg
     return out.value
 
 
-def resolve_algo(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto") -> str:
-    return algo_name(_lib.load().mavg_resolve_algo(n, channels, grade, dtype, _algo_code(algo)))
+def resolve_algo(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto",
+                 library: Optional[str] = None) -> str:
+    lib = _lib.load(library)
+    return lib.mavg_algo_name(lib.mavg_resolve_algo(n, channels, grade, dtype, _algo_code(algo))).decode()
 
 
 def plan(n: int, grade: int, channels: int = 1, dtype: int = F32, algo="auto", block_size: int = 0,

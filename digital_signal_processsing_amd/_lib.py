@@ -60,11 +60,15 @@ EXPORTED_SYMBOLS = (
     "mavg_strerror",
     "mavg_algo_name",
     "mavg_abi_version",
+    "mavg_build_id",
 )
 # exported by the debug build only (include/mavg_debug.h)
 DEBUG_SYMBOLS = ("mavg_test_ahead_schedule",)
-ABI_VERSION = 3
+ABI_VERSION = 4
 DEBUG_LIB_PATH = os.path.join(_PKG, "lib", "libmavg_debug.so")
+# release flags + the test hooks (the forced-schedule parity tests time nothing, but they run the
+# release code paths: no device checks)
+HOOKS_LIB_PATH = os.path.join(_PKG, "lib", "libmavg_hooks.so")
 
 
 class MavgLibraryError(RuntimeError):
@@ -118,6 +122,8 @@ def load(path: str = None) -> ctypes.CDLL:
         lib.mavg_test_ahead_schedule.restype = i
     lib.mavg_abi_version.argtypes = []
     lib.mavg_abi_version.restype = i
+    lib.mavg_build_id.argtypes = []
+    lib.mavg_build_id.restype = ctypes.c_char_p
     _libs[path] = lib
     return lib
 
@@ -131,6 +137,11 @@ def strerror(status: int) -> str:
 
 def algo_name(algo: int) -> str:
     return load().mavg_algo_name(algo).decode()
+
+
+def build_id(path: str = None) -> str:
+    """The source id `path`'s library was compiled from (mavg_build_id)."""
+    return load(path).mavg_build_id().decode()
 
 
 def check(status: int, what: str) -> None:

@@ -196,7 +196,8 @@ template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool
 int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
   constexpr int EPG = 16 / (int)sizeof(T);
   constexpr int NW = WG / 64;
-  constexpr int TF = NW * (64 / C) * Q;  // waves x frame blocks x frames per block
+  constexpr int CL = C * (int)sizeof(T) / 4;  // dword columns per frame (a lane's)
+  constexpr int TF = NW * (64 / CL) * Q;      // waves x frame blocks x frames per block
   constexpr int TG = TF * C / EPG;
   const long long nframes = sg.nframes;
   const long long hg = ((long long)k * C + EPG - 1) / EPG;  // granules covering the k-frame halo
@@ -262,11 +263,9 @@ constexpr size_t ahead_granule_bytes(long long nrec) {
 // slots ahead of its tile) and each run total's (D/8 - 2G) ahead of their
 // consumers; among the J that allow it (up to 8 more than the smallest) the
 // one with the smallest d/G wins.
-#ifndef MAVG_AHEAD_RUN_MAX
-#define MAVG_AHEAD_RUN_MAX 48
-#endif
+constexpr int kAheadRunMax = 48;
 inline int ahead_run_length(long long k, int TF, int ahead) {
-  const int gmax = std::max(2, std::min(MAVG_AHEAD_RUN_MAX, ahead / 20));
+  const int gmax = std::max(2, std::min(kAheadRunMax, ahead / 20));
   const double m = (double)k / TF;
   int J = 1;
   while (m / (8.0 * J) > gmax + 0.5) ++J;
@@ -291,7 +290,9 @@ inline bool ahead_past_l2(long long k, int C, int elem, int TF) {
 }
 template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0, bool HS = false,
           bool RUNS = false, int WG = kWG>
-int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead, bool self = false) {
+// lds_floor: the LDS the launch allocates at least (fewer workgroups per CU, a footprint cap; 0: none)
+int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead, bool self = false,
+                      size_t lds_floor = 0) {
   constexpr int NW = WG / 64;
   const long long nframes = sg.nframes;
   ahead &= ~7;
@@ -318,13 +319,8 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   // XCD -> runs of 64 tiles -> window-matched runs: k=4e6 0.185 -> 0.526;
   // k=1e6 0.524 -> 0.588 -> 0.668; k=6e5 0.594 -> 0.599 -> 0.681
   constexpr int TF = WG * F * U;
-#ifdef MAVG_AHEAD_FIXED_RUN
-  const int xcd_remap = ahead_past_l2(k, C, sizeof(T), TF) ? MAVG_AHEAD_FIXED_RUN : 1;
-  static_assert(!RUNS, "run totals need window-matched runs");
-#else
   const int xcd_remap = ahead_past_l2(k, C, sizeof(T), TF) ? ahead_run_length(k, TF, ahead_plan) : 1;
   if (RUNS && xcd_remap == 1) return MAVG_ERR_UNSUPPORTED;
-#endif
   constexpr int VE = F * C;
   constexpr int NSEG = U * NW;
   using SA = typename ScanAcc<T, A>::type;
@@ -349,9 +345,7 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   size_t lds = kStageBytes + (size_t)NW * C * sizeof(A) + (size_t)(NSEG + 3 * NW) * C * sizeof(SA);
   if (HS) lds = (lds + 15) / 16 * 16 + (size_t)U * WG * VE * sizeof(T);  // + the tile
   if (lds > kLdsBudget) return MAVG_ERR_UNSUPPORTED;
-#ifdef MAVG_AHEAD_LDS_MIN  // tuning builds: fewer workgroups per CU through a bigger LDS allocation
-  lds = std::max<size_t>(lds, MAVG_AHEAD_LDS_MIN);
-#endif
+  lds = std::max(lds, lds_floor);
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
              "ahead_scan<%s,acc=%s,C=%d,F=%d,U=%d,%s,nt=%d,rc=%d,dma=%d,wrec=%d,dv=%d> grid=%lld block=%d lds=%zu "
@@ -402,14 +396,10 @@ int launch_ahead_scan(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
 //     fp32 keeps the tile in registers across the second barrier (RC, fewer
 //     live fp64 accumulators)
 //   otherwise: per-tile records, D = 768 (stereo int16) / 1024
-#ifndef MAVG_AHEAD_WG  // tuning builds: workgroup size of the look-ahead scan (the tile stays U*256 units)
-#define MAVG_AHEAD_WG kWG
-#endif
 template <typename T, typename A, int C, int F, bool HS = false, int U0 = 4>
 int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
-  constexpr int WG = MAVG_AHEAD_WG;
-  constexpr int U = U0 * kWG / WG;
-  static_assert(U >= 1 && U * WG == U0 * kWG, "look-ahead tile of U0 x 256 units");
+  constexpr int WG = kWG;
+  constexpr int U = U0;
   constexpr int TF = WG * F * U;
   constexpr int kNtA = kNtStore | kNtHalo;
   constexpr bool kRC = sizeof(T) == 4 && C == 1 && !HS;
@@ -419,11 +409,7 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   // the records of the few tiles a window spans are out by the time the scan is done (A/B,
   // profiles/r03_tuning/self/: k=5000 0.704 -> 0.734, 8192 0.712 -> 0.735, 12288 0.709 -> 0.728;
   // k=20000 0.712 -> 0.692 and int16 stereo / mono past 3 tiles lose: late neighbours' records)
-#ifdef MAVG_AHEAD_SELF  // tuning builds: 0 never, 1 always (outside the run-total kernel)
-  const bool self = MAVG_AHEAD_SELF != 0;
-#else
   const bool self = sizeof(T) == 4 && C == 1 && !HS && (long long)k <= 3LL * TF;
-#endif
   // 8192-frame tiles (U = 8, 32 KiB) with per-tile records: 3 workgroups per
   // CU with twice the bytes each instead of 5-6 with 16 KiB, and a shorter
   // look-ahead in slots (fp32 D = 320, int16 D = 256) for about the same
@@ -437,25 +423,16 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   //     1e5 0.527 -> 0.572.
   //   int16 mono (16384-frame tiles) lost in the tuner (0.680 -> 0.667).
   // (16-B units only: the frame-unit form of element-aligned views keeps U = 4)
-#ifndef MAVG_AHEAD_NO_U8  // tuning builds: the round-3 4096-frame tiles only (A/B)
-  constexpr bool kU8 = !HS && U0 == 4 && WG == kWG && F * C * (int)sizeof(T) == 16 &&
+  constexpr bool kU8 = !HS && U0 == 4 && F * C * (int)sizeof(T) == 16 &&
                        ((sizeof(T) == 4 && C == 1) || (sizeof(T) == 2 && C == 2));
-#else
-  constexpr bool kU8 = false;
-#endif
   if constexpr (kU8) {
     constexpr int TF8 = WG * F * 8;
     const bool u8 = sizeof(T) == 4 ? !self && ahead_past_l2(k, C, sizeof(T), TF8) && (long long)k <= kAheadU8MaxTiles * TF8
                                    : !(ahead_past_l2(k, C, sizeof(T), TF) && (long long)k > 384LL * TF);
-    // phase A keeps the default policy: non-temporal phase-A loads (kNtPhaseA, tuning builds
-    // -DMAVG_AHEAD_NTA) measured +3-4 % in the in-process tuner but -15 to -18 % in bench.py's
-    // timing (profiles/r04_tuning/u8/nta_*, bench_timing_nta_*: k=4e6 0.620 -> 0.510, 2e6
-    // 0.652 -> 0.546, 1e6 0.660 -> 0.556, 6e5 0.664 -> 0.557)
-#ifdef MAVG_AHEAD_NTA
-    constexpr int kNt8 = sizeof(T) == 4 ? (kNtA | kNtPhaseA) : kNtA;
-#else
+    // phase A keeps the default policy: non-temporal phase-A loads (kNtPhaseA) measured +3-4 % in
+    // the in-process tuner but -15 to -18 % in bench.py's timing (round 4, profiles/r04_tuning/u8/
+    // nta_*, bench_timing_nta_*: k=4e6 0.620 -> 0.510, 2e6 0.652 -> 0.546, 1e6 0.660 -> 0.556)
     constexpr int kNt8 = kNtA;
-#endif
     if (u8) return launch_ahead_scan<T, A, C, F, 8, kNt8, kRC, true, false, 0, false, false, WG>(sg, k, st, ws,
                                                                                               sizeof(T) == 4 ? 320 : 256);
   }
@@ -464,14 +441,12 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   if (wrec) {
     if constexpr (C == 1) s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, true, 0, HS, false, WG>(sg, k, st, ws, 512, self);
   }
-#if !defined(MAVG_AHEAD_FIXED_RUN) && !defined(MAVG_AHEAD_NO_RUNS)
   // run totals (O(J + G) carry items instead of k/T) where the windows are
   // long enough to pay for the kernel's extra registers (4 waves per SIMD
   // instead of 5): > 384 tiles (A/B, profiles/r03_tuning/runs/: fp32
   // k=4e6 0.543 -> 0.596, k=2e6 0.623 -> 0.641; k=1e6 0.670 -> 0.642)
   else if (C <= 2 && U0 == 4 && !HS && ahead_past_l2(k, C, sizeof(T), TF) && (long long)k > 384LL * TF)
     s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS, C <= 2 && U0 == 4 && !HS, WG>(sg, k, st, ws, D);
-#endif
   else
     s = launch_ahead_scan<T, A, C, F, U, kNtA, kRC, true, false, 0, HS, false, WG>(sg, k, st, ws, D, self);
   // the Hillis-Steele form also stages the tile: wide frames (e.g. 8 fp32
@@ -485,11 +460,13 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
 // wide look-ahead scan (mavg_wide.hpp): the look-ahead record carry in its
 // unit layout (F frames x U units per lane, per-tile records) with the wide
 // in-tile scan (P-frame chunks x UW rows); 16-B-aligned views only.
-template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false>
+template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false,
+          bool XG = false, int MW = 0>
 int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
   constexpr int NW = WG / 64;
   constexpr int EPG = 16 / (int)sizeof(T);
-  constexpr int TF = CH ? NW * (64 / C) * P : WG * P * UW;  // CH: P frames of one channel per lane
+  constexpr int CL = C * (int)sizeof(T) / 4 > 0 ? C * (int)sizeof(T) / 4 : 1;  // CH: dword columns per frame
+  constexpr int TF = CH ? NW * (64 / CL) * P : WG * P * UW;  // CH: P frames of one dword column per lane
   constexpr int TG = TF * C / EPG;
   constexpr int NSEG = UW * NW;
   using SA = typename ScanAcc<T, A>::type;
@@ -512,14 +489,16 @@ int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   const long long nfull = nframes / TF;
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
   const size_t need = ahead_granule_bytes<T, A, C, F, U>(nfull);  // per-tile records + 16
-  const size_t lds = (size_t)(2 * TG + 1) * 16 + (size_t)NW * C * sizeof(A) + (size_t)(NSEG + 3 * NW) * C * sizeof(SA);
+  // the shifted tile (+ one granule for an x[n-k] extraction) and, unless XG, the tile
+  const size_t lds = (size_t)((XG ? 1 : 2) * TG + 1) * 16 + (size_t)NW * C * sizeof(A) +
+                     (size_t)(NSEG + 3 * NW) * C * sizeof(SA);
   if (lds > 80 * 1024) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "wide_ahead<%s,acc=%s,C=%d,P=%d,U=%d,nt=%d,dv=%d,F=%d,FU=%d%s> grid=%lld block=%d lds=%zu tile_frames=%d "
-             "ahead=%d remap=%d ws=%zu",
-             type_name<T>(), type_name<A>(), C, P, UW, NT, DV, F, U, CH ? ",ch=1" : "", ntiles, WG, lds, TF, ahead,
-             xcd_remap, need);
+             "wide_ahead<%s,acc=%s,C=%d,P=%d,U=%d,nt=%d,dv=%d,F=%d,FU=%d%s%s,mw=%d> grid=%lld block=%d lds=%zu "
+             "tile_frames=%d ahead=%d remap=%d ws=%zu",
+             type_name<T>(), type_name<A>(), C, P, UW, NT, DV, F, U, CH ? ",ch=1" : "", XG ? ",xg=1" : "", MW, ntiles,
+             WG, lds, TF, ahead, xcd_remap, need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -548,11 +527,11 @@ int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.runs = nullptr;
   p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
   if (lds > 64 * 1024) {
-    const int s = raise_dyn_lds_limit<&wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH>>(80 * 1024);
+    const int s = raise_dyn_lds_limit<&wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH, XG, MW>>(80 * 1024);
     if (s != MAVG_OK) return s;
   }
-  hipLaunchKernelGGL((wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH>), dim3((unsigned)ntiles), dim3(WG), lds, st,
-                     p);
+  hipLaunchKernelGGL((wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH, XG, MW>), dim3((unsigned)ntiles), dim3(WG), lds,
+                     st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
@@ -714,15 +693,16 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 16, 1, kWG, kNtS>(sg, k, st);
     return launch_wide_ahead<T, A, C, 8, 1, kWG, kNtA, 0, 2, 4>(sg, k, st, ws, 512);
   } else if constexpr (sizeof(T) == 4 && C == 4) {
-#ifndef MAVG_NO_CHAN_XG
     // 2048 <= k <= 3584: the halo-only channel-per-lane tile (2048-frame tiles; in-process,
     // profiles/r04_tuning/chan/xg_c4_*, xgr_*: k=2048 0.660 -> 0.712 against the wide tile, 3000
     // 0.541 -> 0.675 against the wide look-ahead; k=4096 ties it, 0.559 vs 0.556)
     if (k >= 2048 && halo_bytes <= 57344) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
-#endif
     if (halo_bytes <= 4096) return launch_wide_tile<T, A, C, 8, 2, kWG, kNtS>(sg, k, st);
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
-    return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 512);
+    // past the halo-only tile: the halo-only channel-per-lane look-ahead, 2048-frame tiles (round 5,
+    // in-process, profiles/r05_tuning/wide/pa0_c4_k44100.log: k=44100 0.540 -> 0.593 against the
+    // chunk look-ahead)
+    return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 8, true, true>(sg, k, st, ws, 512);
   } else if constexpr (sizeof(T) == 4 && C == 8) {
     // one channel per lane (chan_tile_kernel, 32 frames each): one scan per
     // tile row for all 8 channels instead of 8 per chunk (in-process A/B,
@@ -730,44 +710,41 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     // 256 0.705 -> 0.723, 7 0.744 -> 0.778 with 128 threads); past its halo the
     // same in-tile scan in the look-ahead carry (CH): k=2048 0.464 -> 0.488,
     // 4096 0.462 -> 0.487 (128 threads), 44100 0.390 -> 0.433 (256, D = 512)
-#ifndef MAVG_NO_CHAN
     if (halo_bytes <= 256) return launch_chan_tile<T, A, C, 32, 128, kNtS>(sg, k, st);
-#ifndef MAVG_NO_CHAN_XG
     // windows of at least a tile: stage the halo only, x straight from global memory (XG: half
     // the LDS, twice the workgroups per CU; bench timing, profiles/r04_tuning/chan/bench_timing_xg_*:
     // k=1024 0.562 -> 0.737 (1024-frame tiles, bit-identical), 768 0.583 -> 0.647, 512 0.671 ->
     // 0.739 (512-frame tiles); in-process xg_*: 0.563 -> 0.748, 0.582 -> 0.682, 0.675 -> 0.751)
     // up to 64 KiB of halo (k <= 2048), where the wide look-ahead took over (in-process,
     // profiles/r04_tuning/chan/xgr_*: k=1536 0.478 -> 0.656, 2048 0.482 -> 0.548)
-    if (halo_bytes <= 65536 && k >= 1024) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
+    if (halo_bytes <= 49152 && k >= 1024) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
     if (halo_bytes <= 32768 && k >= 512) return launch_chan_tile<T, A, C, 32, 128, kNtS, 0, true>(sg, k, st);
-#endif
     if (halo_bytes <= 32768) return launch_chan_tile<T, A, C, 32, kWG, kNtS>(sg, k, st);
-    if (halo_bytes <= 131072) return launch_wide_ahead<T, A, C, 32, 1, 128, kNtA, 0, 1, 4, true>(sg, k, st, ws, 512);
-    return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 4, true>(sg, k, st, ws, 512);
-#else  // tuning builds: the chunk-per-lane kernels (A/B)
-    if (halo_bytes <= 256) return launch_wide_tile<T, A, C, 4, 1, 128, kNtS>(sg, k, st);
-    if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 4, 1, kWG, kNtS>(sg, k, st);
-    if (halo_bytes <= 131072) return launch_wide_ahead<T, A, C, 4, 1, 128, kNtA, 0, 1, 4>(sg, k, st, ws, 512);
-    return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
-#endif
+    // past it: the halo-only look-ahead (XG: x straight from global memory, only the shifted tile in
+    // LDS, 33 KiB instead of 65 KiB; round 5, in-process, profiles/r05_tuning/wide/pa0_c8_*: k=44100
+    // 0.429 -> 0.589 (D = 384), k=2048 0.534 (the halo-only tile) -> 0.616)
+    return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 4, true, true>(sg, k, st, ws, 384);
   } else if constexpr (sizeof(T) == 2 && C == 4) {
     if constexpr (sizeof(A) == 4) {
       if (halo_bytes <= 8192) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
       if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 16, 1, kWG, kNtS>(sg, k, st);
-#ifndef MAVG_NO_I16C4_WIDE_AHEAD
       // past it the wide look-ahead (64-B chunks, D = 512) instead of the 16-B unit look-ahead
       // (in-process A/B, profiles/r04_tuning/wide/wide_i16_c4_*: k=44100 0.579 -> 0.598, 20000
       // 0.590 -> 0.602; bench timing, bit-exact, profiles/r04_tuning/wide/bench_timing_i16_c4_*:
       // k=44100 0.575 -> 0.586, 60000 0.582 -> 0.591, 20000 0.587 -> 0.590)
       return launch_wide_ahead<T, A, C, 8, 1, kWG, kNtA, 0, 2, 4>(sg, k, st, ws, 512);
-#endif
     }
   } else if constexpr (sizeof(T) == 2 && C == 8) {
     if constexpr (sizeof(A) == 4) {
       if (halo_bytes <= 256) return launch_wide_tile<T, A, C, 8, 1, 128, kNtS>(sg, k, st);
-      if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
+      if (halo_bytes < 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
+      // a window of at least the tile: the halo-only channel-per-lane tile, a dword column (two
+      // channels) per lane (round 5, in-process, profiles/r05_tuning/wide/i16_c8_k2048.log: k=2048
+      // 0.589 -> 0.652 against the wide tile)
+      if (halo_bytes <= 49152) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
     }
+    // past it the halo-only channel-per-lane look-ahead (int32 sums: k <= 65535)
+    if constexpr (sizeof(A) == 4) return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 8, true, true>(sg, k, st, ws, 384);
     return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
   }
   (void)halo_bytes;
@@ -878,11 +855,7 @@ int launch_direct_block(const Sig& sg, int k, int block, hipStream_t st) {
       default: return launch_direct<T, A, C, F, 1, kWG, kNtDirect>(sg, k, st);
     }
   }
-#ifdef MAVG_DIRECT_R1_SHAPE  // tuning builds only: the round-1 shape (one unit per lane, default policy), A/B
-  return launch_direct<T, A, C, F, 1, kWG, 0>(sg, k, st);
-#else
   return launch_direct<T, A, C, F, 2, kWG, kNtDirect>(sg, k, st);
-#endif
 }
 
 // width: 16 (vload4), 8 (vload2) or 0 (one frame per lane); block: the

@@ -277,6 +277,30 @@ __device__ __forceinline__ void tile_record_lean(const T* __restrict__ in, long 
   }
 }
 
+// Channel c of a per-tile record (tile_record_lean's value for that channel,
+// bit for bit: the same additions in the same order), one accumulator and one
+// loaded sample live: the element loads of the rare recompute path set the
+// register allocation of the whole kernel otherwise (the wide look-ahead: 8
+// fp32 channels, 148 -> 128 VGPRs without a unit-wide load and its select chain).
+template <typename T, typename SA, int C, int F, int U, int WG>
+__device__ __forceinline__ SA tile_record_chan_lean(const T* __restrict__ in, long long j, int c, int lane) {
+  constexpr int TF = WG * F * U;
+  SA r = (SA)0;
+#pragma unroll 1
+  for (int wv = 0; wv < WG / 64; ++wv) {
+    SA ls = (SA)0;
+#pragma unroll 1
+    for (int u = 0; u < U; ++u) {
+      const T* px = in + (j * TF + (long long)(u * WG + wv * 64 + lane) * F) * C + c;
+#pragma unroll
+      for (int fr = 0; fr < F; ++fr) ls += to_acc<SA>(px[fr * C]);
+    }
+    const SA rw = readlane(wave_incl_scan(ls), 63);
+    r = wv == 0 ? rw : r + rw;
+  }
+  return r;
+}
+
 // RUNS: the total of run rr (tiles [rs, rs + G), G <= 64) in A, by one wave:
 // lane l takes tile rs + l's per-tile record (its granules, polled like the
 // carry's, recomputed from the input when still untagged), then one DPP wave
@@ -354,7 +378,11 @@ __device__ __forceinline__ void run_total(const T* __restrict__ in, const gran_t
 // HS: the Hillis-Steele flavour of the in-tile scan (the tile kernel's HS
 //     form: the tile is also staged in LDS, lane l holds frames l, l+64, ...
 //     of its 64F-frame wave segment, a 6-step DPP log-step scan per register,
-//     O(n log n) work); the record carry is the same.  RC must be off.
+//     O(n log n) work); the record carry is the same.  RC must be off (round 5:
+//     the log-step scans rebuilt after the carry from the two LDS stages cut the
+//     fp32 registers 120 -> 74 and lost, 0.548 -> 0.513 of peak at k=44100, int16
+//     mono 0.562 -> 0.517, stereo 0.573 -> 0.527: the scans' VALU no longer hides
+//     the record wait; profiles/r05_tuning/hs/).
 // RUNS: window-matched runs only (remap mode G, per-tile records): the carry
 //     reads the totals of the whole runs inside the window (~8J of them)
 //     plus the tile records of the partial runs at its two ends (< 2g),
@@ -372,19 +400,9 @@ __device__ __forceinline__ void run_total(const T* __restrict__ in, const gran_t
 #define MAVG_ANOW() 0ull
 #endif
 
-#ifndef MAVG_AHEAD_RUNS_MINB  // tuning builds: workgroups per CU the RUNS kernel is compiled for
-#define MAVG_AHEAD_RUNS_MINB 1
-#endif
-#ifndef MAVG_AHEAD_MINB_F32  // tuning builds: the same for the other look-ahead kernels, per dtype
-#define MAVG_AHEAD_MINB_F32 1
-#endif
-#ifndef MAVG_AHEAD_MINB_I16
-#define MAVG_AHEAD_MINB_I16 1
-#endif
 template <typename T, typename A, int C, int F, int U, int NT, bool RC = false, bool DMA = true, bool WREC = false,
           int DV = 0, bool HS = false, bool RUNS = false, int WG_ = kWG>
-__global__ __launch_bounds__(WG_, RUNS ? MAVG_AHEAD_RUNS_MINB : (sizeof(T) == 4 ? MAVG_AHEAD_MINB_F32 : MAVG_AHEAD_MINB_I16))
-void ahead_scan_kernel(AheadParams p) {
+__global__ __launch_bounds__(WG_) void ahead_scan_kernel(AheadParams p) {
   static_assert(!(HS && RC), "the Hillis-Steele flavour keeps its per-element prefixes");
   static_assert(!(RUNS && WREC), "run totals sum per-tile records");
   constexpr int WG = WG_;
@@ -488,11 +506,7 @@ void ahead_scan_kernel(AheadParams p) {
   }
   // HS: whole tiles reach the tile stage by LDS-DMA (no tile registers, no
   // ds_write; the scan reads the stage in its transposed order)
-#ifndef MAVG_HS_NODMA
   constexpr bool kHsDma = HS && kDma;
-#else  // tuning builds: the round-3 register-staged HS tile (A/B)
-  constexpr bool kHsDma = false;
-#endif
   const bool hs_dma = kHsDma && tile_full && !eio;
   U_t x[U];
   if (hs_dma) {

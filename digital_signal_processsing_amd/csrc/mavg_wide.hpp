@@ -387,13 +387,36 @@ __device__ __forceinline__ int chan_slot(int g) {
 // since every x[n-k] of the tile then lies in the halo.  Half the LDS at
 // k = TF (C = 8, k = 1024: 32 KiB, four workgroups per CU instead of two);
 // the outputs are staged in the halo region after the last read of it.
+//
+// int16 (round 5, C = 8): a lane owns one DWORD COLUMN of the frame -- two
+// adjacent channels -- so the addressing is exactly fp32 C = 4's (16-B frames,
+// CL = 4 columns, NB = 16 blocks per wave, conflict-free ds_read_b32 of the
+// chan_slot stage), with E = 2 int32 accumulators per lane; one ds_read_b32
+// serves two samples, half the LDS instructions of a lane per channel.
+template <typename T> struct ChanElem;  // a dword of the stage as E samples
+template <> struct ChanElem<float> {
+  static constexpr int E = 1;
+  static __device__ __forceinline__ float get(uint32_t w, int) { return __uint_as_float(w); }
+  static __device__ __forceinline__ uint32_t put(const float (&y)[1]) { return __float_as_uint(y[0]); }
+};
+template <> struct ChanElem<int16_t> {
+  static constexpr int E = 2;
+  static __device__ __forceinline__ int16_t get(uint32_t w, int e) { return (int16_t)(uint16_t)(w >> (16 * e)); }
+  static __device__ __forceinline__ uint32_t put(const int16_t (&y)[2]) {
+    return (uint32_t)(uint16_t)y[0] | ((uint32_t)(uint16_t)y[1] << 16);
+  }
+};
+
 template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false>
 __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
-  static_assert(sizeof(T) == 4 && (C == 4 || C == 8), "fp32 frames of 16 or 32 bytes");
+  using CE = ChanElem<T>;
+  constexpr int E = CE::E;      // samples (channels) per dword
+  constexpr int CL = C / E;     // dword columns per frame
+  static_assert(C % E == 0 && (CL == 4 || CL == 8), "frames of 16 or 32 bytes");
   constexpr int NW = WG / 64;
-  constexpr int NB = 64 / C;    // frame blocks per wave
-  constexpr int GPF = C / 4;    // 16-B granules per frame
-  constexpr int EPG = 4;        // fp32 elements per granule
+  constexpr int NB = 64 / CL;   // frame blocks per wave
+  constexpr int GPF = CL / 4;   // 16-B granules per frame
+  constexpr int EPG = 16 / (int)sizeof(T);  // samples per granule
   static_assert(ilog2c(GPF) + ilog2c(NB) == 4 && Q * GPF >= 16, "the key spans one bank row, outside its bits");
   constexpr int WF = NB * Q;    // frames per wave
   constexpr int TF = NW * WF;   // tile frames
@@ -406,9 +429,9 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   unsigned char* sb = smem;                              // [Hg + TG] swizzled granules
   A* tot = reinterpret_cast<A*>(smem + (Hg + (XG ? 0 : TG)) * 16);  // [NW][C] wave-segment totals
   A* hsum = tot + NW * C;                                // [NW][C] halo partial sums
-  const float* sf = reinterpret_cast<const float*>(sb);
-  // stage element e (frame * C + channel), swizzled
-  auto elem = [&](int e) -> float { return sf[chan_slot<C, Q>(e >> 2) * 4 + (e & 3)]; };
+  const uint32_t* sw32 = reinterpret_cast<const uint32_t*>(sb);
+  // stage dword d (frame * CL + column), swizzled
+  auto dword_at = [&](int d) -> uint32_t { return sw32[chan_slot<CL, Q>(d >> 2) * 4 + (d & 3)]; };
 
   const T* __restrict__ in = static_cast<const T*>(p.in);
   T* __restrict__ out = static_cast<T*>(p.out);
@@ -429,17 +452,23 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   MAVG_DCHECK(!XG || (k >= TF && Hg >= TG), "chan XG window", k, TF);
   const bool tile_full = t0 + TF <= nframes;
   constexpr int kTileStaged = XG ? 0 : TG;  // granules of the tile in the stage
-  const int c = lane & (C - 1);
-  const int b = lane / C;
+  const int c = lane & (CL - 1);  // the lane's dword column: channels c*E .. c*E + E - 1
+  const int b = lane / CL;
   const int jl = w * WF + b * Q;  // tile frame of the lane's first frame
-  T xr[XG ? Q : 1];
+  uint32_t xr[XG ? Q : 1];
   if constexpr (XG) {  // the lane's x, issued before the stage
     if (tile_full) {
+      const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
 #pragma unroll
-      for (int i = 0; i < Q; ++i) xr[i] = in[(t0 + jl + i) * C + c];
+      for (int i = 0; i < Q; ++i) xr[i] = in32[(t0 + jl + i) * CL + c];
     } else {
 #pragma unroll
-      for (int i = 0; i < Q; ++i) xr[i] = load_elem(in, hist, t0 + jl + i, c, C, nframes, k, p.pre);
+      for (int i = 0; i < Q; ++i) {
+        T v[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = load_elem(in, hist, t0 + jl + i, c * E + e, C, nframes, k, p.pre);
+        xr[i] = CE::put(v);
+      }
     }
   }
 
@@ -448,7 +477,7 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
     const T* src0 = in + h0 * C;  // logical granule 0
 #pragma unroll
     for (int i = 0; i < kTileStaged / WG; ++i) {
-      const int gl = chan_slot<C, Q>(Hg + i * WG + tid);  // the logical granule this lane's slot holds
+      const int gl = chan_slot<CL, Q>(Hg + i * WG + tid);  // the logical granule this lane's slot holds
       unsigned char* d = sb + (Hg + i * WG + wq * 64) * 16;
       if constexpr ((NT & kNtSplit) != 0) {
         // the last Hg granules of the tile are the next tile's halo: default policy (L2)
@@ -460,7 +489,7 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
     }
     for (int j0 = 0; j0 < Hg; j0 += WG) {
       const int s = j0 + tid;
-      if (s < Hg) glds16<(NT & kNtHalo) != 0>(src0 + (long long)chan_slot<C, Q>(s) * EPG, sb + (j0 + wq * 64) * 16);
+      if (s < Hg) glds16<(NT & kNtHalo) != 0>(src0 + (long long)chan_slot<CL, Q>(s) * EPG, sb + (j0 + wq * 64) * 16);
     }
   } else {
     // edge tiles: element loads through load_elem (history, peeled head, zeros)
@@ -472,7 +501,7 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
         const int e = gl * EPG + i;
         u.e[i] = load_elem(in, hist, h0 + e / C, e % C, C, nframes, k, p.pre);
       }
-      IO::store(reinterpret_cast<T*>(sb + chan_slot<C, Q>(gl) * 16), u);
+      IO::store(reinterpret_cast<T*>(sb + chan_slot<CL, Q>(gl) * 16), u);
     }
   }
   __syncthreads();
@@ -485,7 +514,7 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
 #pragma unroll
     for (int i = 0; i < EPG; ++i) hs[i] = (A)0;
     for (int gl = g0 + tid; gl < Hg; gl += WG) {
-      const Gr u = IO::load(reinterpret_cast<const T*>(sb + chan_slot<C, Q>(gl) * 16));
+      const Gr u = IO::load(reinterpret_cast<const T*>(sb + chan_slot<CL, Q>(gl) * 16));
 #pragma unroll
       for (int i = 0; i < EPG; ++i)
         if (gl * EPG + i >= e0) hs[i] += to_acc<A>(u.e[i]);
@@ -493,70 +522,93 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
     // element i of this thread's granules is channel (cb + i) mod C (granules WG apart: whole frames)
     const int cb = ((g0 + tid) * EPG) % C;
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
+    for (int ch = 0; ch < C; ++ch) {
       A part = (A)0;
 #pragma unroll
       for (int i = 0; i < EPG; ++i)
-        if (cb + i == c) part += hs[i];
+        if ((cb + i) % C == ch) part += hs[i];
       const A r = readlane(wave_incl_scan(part), 63);
-      if (lane == 0) hsum[w * C + c] = r;
+      if (lane == 0) hsum[w * C + ch] = r;
     }
   }
 
-  // ---- pass 1: the lane's channel over its Q frames; the scan across its NB lanes ----
+  // ---- pass 1: the lane's channels over its Q frames; the scan across its NB lanes ----
   const int f0 = Hf + jl;  // stage frame of the lane's first frame
-  auto xv = [&](int i) -> T {
+  auto xv = [&](int i) -> uint32_t {
     if constexpr (XG) return xr[i];
-    else return elem((f0 + i) * C + c);
+    else return dword_at((f0 + i) * CL + c);
   };
-  A run = (A)0;
+  A run[E];
 #pragma unroll
-  for (int i = 0; i < Q; ++i) run += to_acc<A>(xv(i)) - to_acc<A>(elem((f0 + i - k) * C + c));
-  // Kogge-Stone over the NB blocks: steps of 1, 2, 4 .. blocks = C, 2C, 4C ..
+  for (int e = 0; e < E; ++e) run[e] = (A)0;
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    const uint32_t x = xv(i), xk = dword_at((f0 + i - k) * CL + c);
+#pragma unroll
+    for (int e = 0; e < E; ++e) run[e] += to_acc<A>(CE::get(x, e)) - to_acc<A>(CE::get(xk, e));
+  }
+  // Kogge-Stone over the NB blocks: steps of 1, 2, 4 .. blocks = CL, 2CL, 4CL ..
   // lanes.  Every step crosses 16-lane rows for half the lanes (block b - 1 of
   // an even block lies in the previous row), so row_shr DPP cannot serve it:
   // ds_bpermute (shfl_up), every lane taking part
-  A incl = run;
+  A incl[E];
 #pragma unroll
-  for (int s = C; s < 64; s <<= 1) {
-    A t = shfl_up(incl, s);
-    t = lane >= s ? t : (A)0;
-    incl += t;
+  for (int e = 0; e < E; ++e) {
+    incl[e] = run[e];
+#pragma unroll
+    for (int s = CL; s < 64; s <<= 1) {
+      A t = shfl_up(incl[e], s);
+      t = lane >= s ? t : (A)0;
+      incl[e] += t;
+    }
+    if (b == NB - 1) tot[w * C + c * E + e] = incl[e];  // the wave segment's total of the channel
   }
-  if (b == NB - 1) tot[w * C + c] = incl;  // the wave segment's total of channel c
   __syncthreads();
 
   // ---- carry: halo sum + the earlier waves' segments of this channel, in wave order ----
-  A base = (A)0;
+  A base[E];
 #pragma unroll
-  for (int i = 0; i < NW; ++i) base += hsum[i * C + c];
+  for (int e = 0; e < E; ++e) {
+    const int ch = c * E + e;
+    base[e] = (A)0;
 #pragma unroll
-  for (int i = 0; i < NW - 1; ++i)
-    if (i < wq) base += tot[i * C + c];
-  base += incl - run;
+    for (int i = 0; i < NW; ++i) base[e] += hsum[i * C + ch];
+#pragma unroll
+    for (int i = 0; i < NW - 1; ++i)
+      if (i < wq) base[e] += tot[i * C + ch];
+    base[e] += incl[e] - run[e];
+  }
 
   // ---- pass 2: the prefix rebuilt from the stage, outputs ----
-  T yv[Q];
+  uint32_t yv[Q];
 #pragma unroll
   for (int i = 0; i < Q; ++i) {
-    base += to_acc<A>(xv(i)) - to_acc<A>(elem((f0 + i - k) * C + c));
-    yv[i] = to_out<T, A, DV>(base, p.o);
+    const uint32_t x = xv(i), xk = dword_at((f0 + i - k) * CL + c);
+    T y[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      base[e] += to_acc<A>(CE::get(x, e)) - to_acc<A>(CE::get(xk, e));
+      y[e] = to_out<T, A, DV>(base[e], p.o);
+    }
+    yv[i] = CE::put(y);
   }
   if (!tile_full) {  // the ragged last tile: element stores
     const long long f = t0 + (long long)jl;
 #pragma unroll
     for (int i = 0; i < Q; ++i)
-      if (f + i < nframes) out[(f + i) * C + c] = yv[i];
+      if (f + i < nframes)
+#pragma unroll
+        for (int e = 0; e < E; ++e) out[(f + i) * C + c * E + e] = CE::get(yv[i], e);
     return;
   }
   // ---- outputs through LDS (the stage layout), 1 KiB of contiguous output per store ----
   __syncthreads();  // every read of the stage is done
-  float* sw = reinterpret_cast<float*>(sb);
+  uint32_t* sww = reinterpret_cast<uint32_t*>(sb);
   const int fo = (XG ? 0 : Hf) + jl;  // XG: the outputs take the halo region (Hg >= TG granules)
 #pragma unroll
   for (int i = 0; i < Q; ++i) {
-    const int e = (fo + i) * C + c;
-    sw[chan_slot<C, Q>(e >> 2) * 4 + (e & 3)] = yv[i];
+    const int d = (fo + i) * CL + c;
+    sww[chan_slot<CL, Q>(d >> 2) * 4 + (d & 3)] = yv[i];
   }
   // the wave reads back only its own frames: wave-level ordering suffices
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -569,7 +621,7 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   for (int r = 0; r < WGR / 64; ++r) {
     const int s = rg + r * 64 + lane;  // slot
     const Gr g = IO::load(reinterpret_cast<const T*>(sb + s * 16));
-    IO::template store<(NT & kNtStore) != 0>(ob + (long long)(chan_slot<C, Q>(s) - rg) * EPG, g);
+    IO::template store<(NT & kNtStore) != 0>(ob + (long long)(chan_slot<CL, Q>(s) - rg) * EPG, g);
   }
 }
 
@@ -597,16 +649,30 @@ namespace mavg {
 // the chunks -- lane = b * C + c owns channel c of P (= Q) consecutive frames,
 // one ds_bpermute scan across a channel's lanes, the chan_slot stage layout
 // (UW = 1); the record carry is unchanged.
-template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false>
-__global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
+// XG (round 5, with CH): the tile is not staged -- each lane loads its P values
+// of x straight from global memory (chan_tile_kernel's halo-only form), only
+// the shifted tile is in LDS, and the outputs leave through it after its last
+// read: half the LDS per workgroup (C = 8, 1024-frame tiles: 33 KiB instead of
+// 65 KiB, four workgroups per CU instead of two).
+// MW: the minimum waves per SIMD the register allocation must allow (0: no
+// bound).  The halo-only form is LDS-sized for 4 (C = 8, 256 threads: 33 KiB,
+// four workgroups per CU), which the unbounded schedule misses by converting
+// every loaded value to fp64 at once.
+template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false,
+          bool XG = false, int MW = 0>
+__global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadParams p) {
   constexpr int NW = WG / 64;
   constexpr int EPG = 16 / (int)sizeof(T);
   constexpr int CE = CH ? 4 * C : P * C;   // (CH: unused)
   constexpr int G = CE / EPG;
   static_assert(CE % EPG == 0 && (G == 4 || G == 8), "64-B or 128-B chunks");
-  static_assert(!CH || (sizeof(T) == 4 && UW == 1 && (C == 4 || C == 8)), "channel-per-lane form: fp32, C = 4 or 8");
+  using CEl = ChanElem<T>;                 // CH: a stage dword as E samples (fp32 1, int16 2)
+  constexpr int E = CEl::E;
+  constexpr int CL = C / E > 0 ? C / E : 1;  // CH: dword columns per frame (a lane owns one)
+  static_assert(!CH || (UW == 1 && C % E == 0 && (CL == 4 || CL == 8)), "channel-per-lane form: 16- or 32-B frames");
+  static_assert(!XG || CH, "the halo-only form is the channel-per-lane form's");
   constexpr int QM = G == 4 ? 3 : 7;
-  constexpr int NB = 64 / C;               // CH: frame blocks per wave
+  constexpr int NB = 64 / CL;              // CH: frame blocks per wave
   constexpr int WF = NB * P;               // CH: frames per wave
   constexpr int TF = CH ? NW * WF : WG * P * UW;
   static_assert(TF == WG * F * U, "the record units tile the same frames as the chunks");
@@ -621,9 +687,9 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
   constexpr int NG = GranCount<SA>::n;
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* sstage = smem;              // [SG] shifted tile, swizzled granules
-  unsigned char* tstage = smem + SG * 16;    // [TG] the tile, swizzled granules (then the outputs)
-  A* hsum = reinterpret_cast<A*>(tstage + TG * 16);  // [NW][C]
+  unsigned char* sstage = smem;              // [SG] shifted tile, swizzled granules (XG: then the outputs)
+  unsigned char* tstage = smem + SG * 16;    // [TG] the tile, swizzled granules (then the outputs); XG: absent
+  A* hsum = reinterpret_cast<A*>(tstage + (XG ? 0 : TG) * 16);  // [NW][C]
   SA* tot = reinterpret_cast<SA*>(hsum + NW * C);    // [NSEG][C]
   SA* shares = tot + NSEG * C;                         // [3][NW][C]
 
@@ -653,7 +719,7 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
   const long long nitem = qhi - qlo;
 
   auto slot = [](int g) -> int {
-    if constexpr (CH) return chan_slot<C, P>(g);
+    if constexpr (CH) return chan_slot<CL, P>(g);
     else return stage_slot<QM>(g);
   };
   // ---- 1. the tile and the shifted tile to LDS; phase A; own / head-duty records ----
@@ -661,7 +727,36 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
   const unsigned bd = blockIdx.x + (unsigned)p.ahead;
   const long long ja = bd < nb ? map_tile(bd) : -1;
   const bool produce = ja >= 0 && ja < p.nfull;
-  if (tile_full) {
+  // XG: the lane's x (dword column cl -- channels cl*E .. cl*E + E - 1 -- of frames j0 .. j0 + P - 1)
+  const int cl = lane & (CL - 1);  // CH: the lane's dword column
+  const int j0 = w * WF + (lane / CL) * P;
+  uint32_t xr[XG ? P : 1];
+  auto load_x = [&]() {
+    if (tile_full) {
+      const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
+#pragma unroll
+      for (int i = 0; i < P; ++i) xr[i] = in32[(t0 + j0 + i) * CL + cl];
+    } else {
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        T v[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = load_elem(in, hist, t0 + j0 + i, cl * E + e, C, nframes, k, pre);
+        xr[i] = CEl::put(v);
+      }
+    }
+  };
+  // XG: x first of all (round 5, in-process A/B, profiles/r05_tuning/wide/xgat_*: loaded after the
+  // first barrier, or after the record carry with the in-tile scan moved there -- 118 instead of 150
+  // VGPRs for 8 channels -- both slower: C = 8, k = 44100 0.570 -> 0.518 / 0.487; the tile's x
+  // latency then lies on the tile's path)
+  if constexpr (XG) load_x();
+  // phase A's tile (its loads issued after the stage: issued first they measured 0.581 -> 0.534 for
+  // 8 channels at k = 44100, profiles/r05_tuning/wide/pa_*)
+  Unit<T, VE> xa[U];
+  if (XG) {
+    // no tile stage
+  } else if (tile_full) {
     const T* src = in + t0 * C;
 #pragma unroll
     for (int i = 0; i < TG / WG; ++i) {
@@ -706,7 +801,6 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
     }
   };
   if (produce) {  // phase A: tile t + D, default policy (its own later loads hit L2)
-    Unit<T, VE> xa[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) xa[u] = IO::gload(in + (ja * TF + (long long)(u * WG + tid) * F) * C, false);
     SA r[C];
@@ -750,20 +844,32 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
     for (int h = 0; h < NG; ++h) rv[h] = 0ull;
   }
   __syncthreads();
-  if (w < 3) {
-    const long long j = w == 0 ? (produce ? ja : -1) : (w == 1 ? (own ? tile : -1) : jh);
-    if (j >= 0) publish_record_lds<SA, C, NW>(gran, j, shares + (w * NW) * C, lane);
+  // the three record sources (phase A, own tile, head duty), one per wave: a
+  // loop, so a 2-wave workgroup (128 threads) publishes its head-duty records too
+  for (int src = wq; src < 3; src += NW) {
+    const long long j = src == 0 ? (produce ? ja : -1) : (src == 1 ? (own ? tile : -1) : jh);
+    if (j >= 0) publish_record_lds<SA, C, NW>(gran, j, shares + (src * NW) * C, lane);
   }
 
   // ---- 2. the partial window before frame 0 (history / peeled head) ----
-  A hp[C];
+  // (CH: each thread sums its own channel cc only -- one accumulator held
+  // across the scan and the carry instead of C)
+  constexpr int HPC = CH ? 1 : C;
+  A hp[HPC];
 #pragma unroll
-  for (int c = 0; c < C; ++c) hp[c] = (A)0;
+  for (int c = 0; c < HPC; ++c) hp[c] = (A)0;
   if (a < 0 && (hist != nullptr || pre > 0)) {
+    if constexpr (CH) {
+      // element e of the window before frame 0 is (frame a + e / C, channel e mod C); a
+      // thread's elements are WG apart, a multiple of C: all of channel cc = tid mod C
 #pragma unroll 1
-    for (long long f = a + tid; f < 0; f += WG)
+      for (long long e = tid; e < -a * C; e += WG) hp[0] += to_acc<A>(load_elem(in, hist, a + e / C, cc, C, nframes, k, pre));
+    } else {
+#pragma unroll 1
+      for (long long f = a + tid; f < 0; f += WG)
 #pragma unroll
-      for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(load_elem(in, hist, f, c, C, nframes, k, pre));
+        for (int c = 0; c < C; ++c) hp[c] += to_acc<A>(load_elem(in, hist, f, c, C, nframes, k, pre));
+    }
   }
 
   // ---- 3. the wide in-tile scan; the partial window [a, jlo T) is the x[n-k]
@@ -803,31 +909,65 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
   };
   // CH: the lane's channel over its P frames, then the scan across the NB
   // lanes of the channel (chan_tile_kernel); the partial window's x[n-k] of
-  // the lane's channel in hpo
-  const int cl = lane & (C - 1);  // CH: the lane's channel (= cc: WG is a multiple of C)
-  const int j0 = w * WF + (lane / C) * P;
-  const float* tsf = reinterpret_cast<const float*>(tstage);
-  const float* ssf = reinterpret_cast<const float*>(sstage);
-  auto tel = [&](int e) -> float { return tsf[chan_slot<C, P>(e >> 2) * 4 + (e & 3)]; };
-  auto sel = [&](int e) -> float { return ssf[chan_slot<C, P>(e >> 2) * 4 + (e & 3)]; };
-  SA crun = (SA)0, cincl = (SA)0;
-  A hpo = (A)0;
-  if constexpr (CH) {
+  // the lane's channel in hpo.
+  // Stage addressing (F = 1, so Ha = k: x[n-k] of tile frame f is shifted-
+  // stage frame f, the tile stage's frame f is x): element (j0 + i, cl) lies in
+  // chan_slot granule j0 GPF + ((i ^ bq) << LG) + cl/4 (the key of chan_slot is
+  // the lane's block bq for every i < P), i.e. at float index
+  // tb[i mod NBX] + (i / NBX) * NBX * 4 GPF with a table of NBX lane offsets --
+  // NBX address registers instead of the P the compiler would otherwise keep
+  // live from pass 1 to pass 2.
+  const uint32_t* tsf = reinterpret_cast<const uint32_t*>(tstage);
+  const uint32_t* ssf = reinterpret_cast<const uint32_t*>(sstage);
+  constexpr int GPFc = CL >= 4 ? CL / 4 : 1;
+  constexpr int NBX = NB < P ? NB : P;
+  constexpr int kFS = 4 * GPFc;  // floats per frame of the stage
+  auto ch_table = [&](int lb, int bq, int (&tb)[NBX]) {
+#pragma unroll
+    for (int r = 0; r < NBX; ++r) tb[r] = lb + (r ^ bq) * kFS;
+  };
+  auto ch_idx = [&](const int (&tb)[NBX], int i) -> int { return tb[i % NBX] + (i / NBX) * NBX * kFS; };
+  const int ch_lb = (j0 * GPFc + (cl >> 2)) * 4 + (cl & 3);  // frame j0 before the key
+  constexpr int kGrp = 8;  // frames per scheduling group of the two passes (sched_barrier between groups)
+  const int ch_bq = lane / CL;
+  SA crun[E], cincl[E];  // CH: per channel of the lane's column
+  A hpo[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) crun[e] = cincl[e] = (SA)0, hpo[e] = (A)0;
+  auto ch_pass1 = [&]() {
+    static_assert(!CH || (F == 1 && NBX * (P / NBX) == P), "Ha = k: x[n-k] of tile frame f is shifted-stage frame f");
+    MAVG_DCHECK(Ha == k, "CH shifted stage offset", Ha, k);
+    int tb[NBX];
+    ch_table(ch_lb, ch_bq, tb);
 #pragma unroll
     for (int i = 0; i < P; ++i) {
-      const float xk = sel((Ha - k + j0 + i) * C + cl);
-      if (j0 + i < pcount) hpo += to_acc<A>(xk);
-      crun += to_acc<SA>(tel((j0 + i) * C + cl)) - to_acc<SA>(xk);
-    }
-    cincl = crun;
+      // groups of kGrp frames the scheduler may not mix: bounded live fp64 conversions
+      if (i % kGrp == 0 && i > 0) __builtin_amdgcn_sched_barrier(0);
+      const int ix = ch_idx(tb, i);
+      MAVG_DCHECK((ix == (chan_slot<CL, P>(((j0 + i) * CL + cl) >> 2) * 4 + (cl & 3))), "CH stage index", ix, i);
+      const uint32_t xk = ssf[ix];
+      uint32_t xv;
+      if constexpr (XG) xv = xr[i];
+      else xv = tsf[ix];
 #pragma unroll
-    for (int sh = C; sh < 64; sh <<= 1) {
-      SA t = shfl_up(cincl, sh);
-      t = lane >= sh ? t : (SA)0;
-      cincl += t;
+      for (int e = 0; e < E; ++e) {
+        if (j0 + i < pcount) hpo[e] += to_acc<A>(CEl::get(xk, e));
+        crun[e] += to_acc<SA>(CEl::get(xv, e)) - to_acc<SA>(CEl::get(xk, e));
+      }
     }
-    if (lane >= 64 - C) tot[w * C + cl] = cincl;
-  }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      cincl[e] = crun[e];
+#pragma unroll
+      for (int sh = CL; sh < 64; sh <<= 1) {
+        SA t = shfl_up(cincl[e], sh);
+        t = lane >= sh ? t : (SA)0;
+        cincl[e] += t;
+      }
+      if (lane >= 64 - CL) tot[w * C + cl * E + e] = cincl[e];
+    }
+  };
+  if constexpr (CH) ch_pass1();
   SA lx[UW][C];
 #pragma unroll
   for (int uw = 0; uw < UW && !CH; ++uw) {
@@ -892,14 +1032,16 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
     while (mask != 0ull) {
       const int l = __builtin_ctzll(mask);
       const long long ql = __shfl(sl, l, 64) / C;
-      SA r[C];
-      tile_record_lean<T, SA, C, F, U, WG>(in, qlo + ql, lane, false, r);
+      // one channel at a time (the producer's additions for that channel, the
+      // same bits): one accumulator live instead of a whole record's C
+      SA v = (SA)0;
+#pragma unroll 1
+      for (int c = 0; c < C; ++c) {
+        const SA rc = tile_record_chan_lean<T, SA, C, F, U, WG>(in, qlo + ql, c, lane);
+        if (cc == c) v = rc;
+      }
       const bool mine = miss && sl / C == ql;
       if (mine) {
-        SA v = r[0];
-#pragma unroll
-        for (int c = 1; c < C; ++c)
-          if (cc == c) v = r[c];
 #pragma unroll
         for (int h = 0; h < NG; ++h) rv[h] = kGranTag | gran_word(v, h);
       }
@@ -914,40 +1056,74 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
   }
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    const A r = readlane(wave_incl_scan(hp[c] + (cc == c ? hq + hpo : (A)0)), 63);
+    A part;
+    if constexpr (CH) {
+      part = cc == c ? hp[0] + hq : (A)0;
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (cl * E + e == c) part += hpo[e];
+    }
+    else part = hp[c] + (cc == c ? hq : (A)0);
+    const A r = readlane(wave_incl_scan(part), 63);
     if (lane == 0) hsum[w * C + c] = r;
   }
   __syncthreads();
 
   // ---- 5. carry + earlier segments; pass 2 rebuilt from the stages; outputs ----
   if constexpr (CH) {
-    A base = (A)0;
+    A base[E];
 #pragma unroll
-    for (int i = 0; i < NW; ++i) base += hsum[i * C + cl];
+    for (int e = 0; e < E; ++e) {
+      const int ch = cl * E + e;
+      base[e] = (A)0;
 #pragma unroll
-    for (int i = 0; i < NW - 1; ++i)
-      if (i < wq) base += (A)tot[i * C + cl];
-    base += (A)(cincl - crun);
-    T yv[P];
-    SA run = (SA)0;
+      for (int i = 0; i < NW; ++i) base[e] += hsum[i * C + ch];
+#pragma unroll
+      for (int i = 0; i < NW - 1; ++i)
+        if (i < wq) base[e] += (A)tot[i * C + ch];
+      base[e] += (A)(cincl[e] - crun[e]);
+    }
+    // the address table again, from values the compiler cannot prove equal to
+    // pass 1's (it would keep pass 1's P addresses live across the carry)
+    int lb2 = ch_lb, bq2 = ch_bq;
+    asm volatile("" : "+v"(lb2), "+v"(bq2));
+    if constexpr (XG) {
+      // likewise x: without this the compiler keeps pass 1's fp64 conversions
+      // of the P values (2 P registers) live across the carry instead of x (P)
+#pragma unroll
+      for (int i = 0; i < P; ++i) asm volatile("" : "+v"(xr[i]));
+    }
+    int tb[NBX];
+    ch_table(lb2, bq2, tb);
+    // each output replaces, in the shifted stage, the x[n-k] it was the last
+    // read of (the same lane, the same address: no barrier); the wave then
+    // reads its own frames back slot-contiguous
+    uint32_t* sw = reinterpret_cast<uint32_t*>(sstage);
+    SA run[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) run[e] = (SA)0;
 #pragma unroll
     for (int i = 0; i < P; ++i) {
-      run += to_acc<SA>(tel((j0 + i) * C + cl)) - to_acc<SA>(sel((Ha - k + j0 + i) * C + cl));
-      yv[i] = to_out<T, A, DV>(base + (A)run, p.o);
-    }
-    if (!tile_full) {
+      if (i % kGrp == 0 && i > 0) __builtin_amdgcn_sched_barrier(0);
+      const int ix = ch_idx(tb, i);
+      const uint32_t xk = sw[ix];
+      uint32_t xv;
+      if constexpr (XG) xv = xr[i];
+      else xv = tsf[ix];
+      T y[E];
 #pragma unroll
-      for (int i = 0; i < P; ++i)
-        if (t0 + j0 + i < nframes) out[(t0 + j0 + i) * C + cl] = yv[i];
-      return;
-    }
-    __syncthreads();  // every read of the tile stage is done: it takes the outputs
-    float* tw = reinterpret_cast<float*>(tstage);
+      for (int e = 0; e < E; ++e) {
+        run[e] += to_acc<SA>(CEl::get(xv, e)) - to_acc<SA>(CEl::get(xk, e));
+        y[e] = to_out<T, A, DV>(base[e] + (A)run[e], p.o);
+      }
+      if (tile_full) {
+        sw[ix] = CEl::put(y);
+      } else if (t0 + j0 + i < nframes) {
 #pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const int e = (j0 + i) * C + cl;
-      tw[chan_slot<C, P>(e >> 2) * 4 + (e & 3)] = yv[i];
+        for (int e = 0; e < E; ++e) out[(t0 + j0 + i) * C + cl * E + e] = y[e];
+      }
     }
+    if (!tile_full) return;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -957,8 +1133,8 @@ __global__ __launch_bounds__(WG) void wide_ahead_kernel(AheadParams p) {
 #pragma unroll
     for (int r = 0; r < WGR / 64; ++r) {
       const int s2 = rg + r * 64 + lane;
-      const Gr g = GIO::load(reinterpret_cast<const T*>(tstage + s2 * 16));
-      GIO::template store<(NT & kNtStore) != 0>(ob + (long long)(chan_slot<C, P>(s2) - rg) * EPG, g);
+      const Gr g = GIO::load(reinterpret_cast<const T*>(sstage + s2 * 16));
+      GIO::template store<(NT & kNtStore) != 0>(ob + (long long)(chan_slot<CL, P>(s2) - rg) * EPG, g);
     }
     return;
   }

@@ -52,7 +52,8 @@
 extern "C" {
 #endif
 
-#define MAVG_ABI_VERSION 3  /* 2: mavg_plan takes block_size; 3: the schedule test hook moved to mavg_debug.h */
+#define MAVG_ABI_VERSION 4  /* 2: mavg_plan takes block_size; 3: the schedule test hook moved to mavg_debug.h;
+                               4: mavg_build_id */
 
 typedef enum {
     MAVG_I16 = 0, /* int16 PCM in/out (the reference's WAV data path) */
@@ -147,6 +148,10 @@ int mavg_stream_copy(const void* d_in, void* d_out, size_t bytes, void* stream);
 const char* mavg_strerror(int status);
 const char* mavg_algo_name(int algo);
 int mavg_abi_version(void);
+/* Source id the library was compiled from: 16 hex digits of a SHA-256 over
+ * csrc/ and include/ (digital_signal_processsing_amd/build_id.py, linked in by
+ * csrc/Makefile).  Lets a caller prove the loaded library is the tree's. */
+const char* mavg_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -25,7 +25,7 @@ def test_library_exports_every_symbol():
     lib = _lib.load()
     for name in _header_symbols():
         assert hasattr(lib, name), name
-    assert lib.mavg_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.mavg_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_release_library_has_no_test_hook():
@@ -39,6 +39,33 @@ def test_release_library_has_no_test_hook():
     for name in _header_symbols() + _header_symbols("mavg_debug.h"):
         assert hasattr(dbg, name), name
     assert dbg.mavg_abi_version() == _lib.ABI_VERSION
+
+
+def test_loaded_libraries_are_built_from_this_tree():
+    """Every shipped build of the library carries the source id of csrc/ and
+    include/ it was compiled from (mavg_build_id, build_id.py): a prebuilt
+    library that does not match the tree's sources fails here."""
+    from digital_signal_processsing_amd import build_id
+    want = build_id.source_id()
+    assert re.fullmatch(r"[0-9a-f]{16}", want)
+    for path in (_lib.LIB_PATH, _lib.DEBUG_LIB_PATH, _lib.HOOKS_LIB_PATH):
+        assert _lib.build_id(path) == want, (path, "stale library: rebuild with __graft_entry__.build()")
+
+
+def test_build_id_follows_the_sources(tmp_path):
+    """The id changes with any byte of a source file, and only with the sources."""
+    import shutil
+    from digital_signal_processsing_amd import build_id
+    for rel in ("digital_signal_processsing_amd/csrc", "include"):
+        shutil.copytree(os.path.join(ROOT, rel), tmp_path / rel,
+                        ignore=shutil.ignore_patterns("*.o", "*.so", "__pycache__"))
+    base = build_id.source_id(str(tmp_path))
+    assert base == build_id.source_id()
+    (tmp_path / "README").write_text("not a source")
+    assert build_id.source_id(str(tmp_path)) == base
+    hpp = tmp_path / "digital_signal_processsing_amd" / "csrc" / "mavg_tile.hpp"
+    hpp.write_bytes(hpp.read_bytes() + b"\n")
+    assert build_id.source_id(str(tmp_path)) != base
 
 
 def test_strerror_and_names():
@@ -128,9 +155,16 @@ def test_plan_describes_launch_without_gpu():
     assert dsp.plan(1 << 30, 1024, channels=4).startswith("wide_tile<f32,acc=f64,C=4,P=8,U=1")
     assert dsp.plan(1 << 30, 1024, channels=8).startswith("chan_tile<f32,acc=f64,C=8,Q=32")  # a channel per lane
     assert ",xg=1>" in dsp.plan(1 << 30, 1024, channels=8) and ",xg=1>" not in dsp.plan(1 << 30, 511, channels=8)
-    assert dsp.plan(1 << 30, 2049, channels=8).startswith("wide_ahead<f32,acc=f64,C=8,P=32") and ",ch=1>" in dsp.plan(
-        1 << 30, 2049, channels=8)
-    assert ",xg=1>" in dsp.plan(1 << 30, 2048, channels=8) and ",xg=1>" in dsp.plan(1 << 30, 3000, channels=4)
+    # past the halo-only tile (8 channels k > 1536, 4 channels k > 3584): the halo-only channel-per-lane
+    # look-ahead (x from global memory, only the shifted tile in LDS)
+    for C, k in ((8, 1537), (8, 44100), (4, 3585), (4, 44100)):
+        p = dsp.plan(1 << 30, k, channels=C)
+        assert p.startswith(f"wide_ahead<f32,acc=f64,C={C},P=32") and ",ch=1,xg=1," in p, p
+    assert ",xg=1>" in dsp.plan(1 << 30, 1536, channels=8) and ",xg=1>" in dsp.plan(1 << 30, 3000, channels=4)
+    # int16 8 channels: a dword column (two channels) per lane from a window of one tile on
+    i16c8 = lambda k: dsp.plan(1 << 30, k, channels=8, dtype=dsp.I16)
+    assert i16c8(1024).startswith("wide_tile<i16") and i16c8(2048).startswith("chan_tile<i16,acc=i32,C=8,Q=32")
+    assert i16c8(44100).startswith("wide_ahead<i16,acc=i32,C=8,P=32") and ",ch=1,xg=1," in i16c8(44100)
     assert dsp.plan(3 << 28, 1024, channels=3).startswith("tile_scan<f32")  # 12-B frames: frame units
     assert dsp.plan(1 << 30, 1024, channels=2, algo="hillis").startswith("tile_scan<")
     # int16 keeps the register-staged tiles (bench.py's timing, tools/tune/ab_libs.py)

@@ -32,7 +32,7 @@ def test_debug_library_exports_the_abi():
         cwd=ROOT, env=dict(os.environ, MAVG_LIBRARY=DEBUG_LIB), capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     path, ver, ok, plan = r.stdout.split("\n")[:4]
-    assert path == DEBUG_LIB and ver == "3" and ok == "True" and plan.startswith("ahead_scan<"), r.stdout
+    assert path == DEBUG_LIB and ver == "4" and ok == "True" and plan.startswith("ahead_scan<"), r.stdout
 
 
 CHILD = r'''
@@ -112,6 +112,11 @@ for C, k, kern in ((8, 1024, "chan_tile<"), (8, 5, "chan_tile<"), (8, 3000, "wid
     xf = oracle.synth_f32(300_007 * C, seed=8, dist=1)
     y, rf = run(xf, k, C, "auto").astype(np.float64), oracle.mavg_f32(xf, k, C).astype(np.float64)
     assert (np.abs(y - rf) <= 1e-5 * np.maximum(np.abs(rf), 1e-30)).all(), (C, k)
+# int16 with 8 channels: the dword-column (two channels per lane) chan tile and look-ahead
+for k, kern in ((2048, "chan_tile<i16"), (3000, "chan_tile<i16"), (20_000, "wide_ahead<i16")):
+    assert dsp.plan(100_003 * 8, k, 8, dsp.I16).startswith(kern), k
+    xs = oracle.synth_i16(100_003 * 8, seed=k)
+    assert np.array_equal(run(xs, k, 8, "auto"), oracle.mavg_i16(xs, k, 8)), k
 torch.cuda.synchronize()
 print("debug build ok")
 '''

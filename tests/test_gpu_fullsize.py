@@ -33,6 +33,16 @@ CONFIGS = [
     ("f32_stereo_2p30_k1024", 1 << 30, 1024, 2, "f32", "blelloch"),  # fp32 form of the stereo harness layout
     ("f32_c4_2p30_k1024", 1 << 30, 1024, 4, "f32", "blelloch"),
     ("f32_c8_2p30_k1024", 1 << 30, 1024, 8, "f32", "blelloch"),
+    # multi-channel windows past the LDS-staged halo (wide look-ahead) and the halo-only chan tile's edge
+    ("f32_stereo_2p30_k44100", 1 << 30, 44100, 2, "f32", "blelloch"),
+    ("f32_c4_2p30_k44100", 1 << 30, 44100, 4, "f32", "blelloch"),
+    ("f32_c8_2p30_k44100", 1 << 30, 44100, 8, "f32", "blelloch"),
+    ("f32_c8_2p30_k2048", 1 << 30, 2048, 8, "f32", "blelloch"),
+    # the reference's int16 PCM at 4 and 8 channels (wav_header.h:26-48)
+    ("i16_c4_2p30_k1024", 1 << 30, 1024, 4, "i16", "blelloch"),
+    ("i16_c8_2p30_k1024", 1 << 30, 1024, 8, "i16", "blelloch"),
+    ("i16_c4_2p30_k44100", 1 << 30, 44100, 4, "i16", "blelloch"),
+    ("i16_c8_2p30_k44100", 1 << 30, 44100, 8, "i16", "blelloch"),
 ]
 
 

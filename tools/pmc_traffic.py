@@ -65,7 +65,8 @@ def plan_key(plan):
         args = (T, acc, kv["C"], kv["Q"], wg, kv["nt"], kv.get("dv", "0"), "true" if kv.get("xg", "0") == "1" else "false")
     elif fam == "wide_ahead":
         args = (T, acc, kv["C"], kv["P"], kv["U"], wg, kv["nt"], kv.get("dv", "0"), kv["F"], kv["FU"],
-                "true" if kv.get("ch", "0") == "1" else "false")
+                "true" if kv.get("ch", "0") == "1" else "false", "true" if kv.get("xg", "0") == "1" else "false",
+                kv.get("mw", "0"))
     else:
         args = (T, acc)
     return FAMILY[fam], args

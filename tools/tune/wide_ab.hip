@@ -5,7 +5,7 @@
 // checked against the library's (|dy| <= 1e-6 |y|, fp64 sums in another order).
 //
 // build: make -C tools/tune wide_ab
-// run:   tools/tune/wide_ab <log2n> <k> <C> [rounds] [dist] [f32|i16]
+// run:   tools/tune/wide_ab <log2n> <k> <C> [rounds] [dist] [f32|i16] [hs]
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -78,12 +78,35 @@ void addU(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
 }
 
 // the wide look-ahead scan with the channel-per-lane in-tile scan (CH)
-template <typename T, typename A, int C, int Q, int WG, int F, int U>
+template <typename T, typename A, int C, int Q, int WG, int F, int U, bool XG = false, int MW = 0>
 void addAC(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
   constexpr int kNtA = kNtStore | kNtHalo;
   char name[80];
-  snprintf(name, sizeof name, "wahead chan Q%d %d F%d U%d D%d", Q, WG, F, U, D);
-  vs.push_back({name, [=](hipStream_t s) { return launch_wide_ahead<T, A, C, Q, 1, WG, kNtA, 0, F, U, true>(sg, k, s, ws, D); }, {}});
+  snprintf(name, sizeof name, "wahead chan Q%d %d F%d U%d D%d xg%d mw%d", Q, WG, F, U, D, (int)XG, MW);
+  vs.push_back({name, [=](hipStream_t s) {
+                  return launch_wide_ahead<T, A, C, Q, 1, WG, kNtA, 0, F, U, true, XG, MW>(sg, k, s, ws, D);
+                }, {}});
+}
+
+// the Hillis-Steele look-ahead (mono / stereo) at several look-ahead distances; per-wave records
+// for mono as dispatched.  (Round 5 also measured the log-step scans rebuilt after the carry, RC:
+// fewer registers, slower -- profiles/r05_tuning/hs/; the kernel no longer has that form.)
+template <typename T, typename A, int C, int F, bool WREC>
+void addH(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
+  constexpr int kNtA = kNtStore | kNtHalo;
+  char name[80];
+  snprintf(name, sizeof name, "hillis ahead wrec=%d D%d", (int)WREC, D);
+  vs.push_back({name, [=](hipStream_t s) {
+                  return launch_ahead_scan<T, A, C, F, 4, kNtA, false, true, WREC, 0, true, false, 256>(sg, k, s, ws, D);
+                }, {}});
+}
+template <typename T, typename A, int C>
+void add_hs(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
+  constexpr int F = 16 / (C * (int)sizeof(T));
+  for (int D : {384, 512, 768}) {
+    if constexpr (C == 1) addH<T, A, C, F, true>(vs, sg, k, ws, D);
+    else addH<T, A, C, F, false>(vs, sg, k, ws, D);
+  }
 }
 
 template <int C>
@@ -117,15 +140,22 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 512);
     } else if constexpr (C == 4) {
       addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws, 512);
-      addAC<T, A, C, 16, 256, 1, 4>(vs, sg, k, ws, 512);
-      addAC<T, A, C, 32, 256, 1, 8>(vs, sg, k, ws, 512);
+      // the halo-only (XG) channel-per-lane look-ahead
+      addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 384);
+      addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 768);
+      addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 1024);
+      addAC<T, A, C, 16, 256, 1, 4, true, 5>(vs, sg, k, ws, 1024);
+      addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 512);
     } else {
-      addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws);
-      addA<T, A, C, 4, 1, 128, 1, 4>(vs, sg, k, ws, 512);
-      addAC<T, A, C, 32, 256, 1, 4>(vs, sg, k, ws, 1024);
       addAC<T, A, C, 32, 256, 1, 4>(vs, sg, k, ws, 512);
-      addAC<T, A, C, 32, 128, 1, 4>(vs, sg, k, ws, 512);
-      addAC<T, A, C, 16, 256, 1, 2>(vs, sg, k, ws, 1024);
+      // the halo-only (XG) channel-per-lane look-ahead
+      addAC<T, A, C, 32, 256, 1, 4, true>(vs, sg, k, ws, 256);
+      addAC<T, A, C, 32, 256, 1, 4, true>(vs, sg, k, ws, 384);
+      addAC<T, A, C, 32, 256, 1, 4, true>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 32, 256, 1, 4, true>(vs, sg, k, ws, 768);
+      addAC<T, A, C, 32, 128, 1, 4, true>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 16, 256, 1, 2, true>(vs, sg, k, ws, 512);
     }
     if (k > 4096) return;
   }
@@ -175,7 +205,12 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
       addA<T, A, C, 16, 1, 256, 4, 4>(vs, sg, k, ws, 512);
     } else {
       addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws, 1024);
-      addA<T, A, C, 8, 1, 256, 1, 8>(vs, sg, k, ws, 1024);
+      // the halo-only channel-per-lane look-ahead with a dword column (2 channels) per lane
+      addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 256);
+      addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 384);
+      addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 768);
     }
     return;
   }
@@ -187,10 +222,15 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     add1<T, A, C, 16, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 8, 2, 256, 0>(vs, sg, k);
   } else if constexpr (C == 8) {
-    add1<T, A, C, 4, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 8, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 4, 2, 256, 0>(vs, sg, k);
-    add1<T, A, C, 8, 1, 128, 0>(vs, sg, k);
+    // the channel-per-lane tile with two channels (a dword column) per lane
+    addC<T, A, C, 32, 256>(vs, sg, k);
+    addC<T, A, C, 16, 256>(vs, sg, k);
+    addC<T, A, C, 16, 128>(vs, sg, k);
+    addC<T, A, C, 16, 256, true>(vs, sg, k);
+    addC<T, A, C, 32, 256, true>(vs, sg, k);
+    addC<T, A, C, 16, 128, true>(vs, sg, k);
   }
 }
 
@@ -201,6 +241,8 @@ int main(int argc, char** argv) {
   const int rounds = argc > 4 ? atoi(argv[4]) : 6;
   const int dist = argc > 5 ? atoi(argv[5]) : 1;
   const bool i16 = argc > 6 && std::string(argv[6]) == "i16";
+  const bool hs = argc > 7 && std::string(argv[7]) == "hs";  // the Hillis-Steele look-ahead forms
+  const int algo = hs ? MAVG_ALGO_HILLIS : MAVG_ALGO_BLELLOCH;
   const int dt = i16 ? MAVG_I16 : MAVG_F32;
   const int eb = i16 ? 2 : 4;
   const int steps = 10;
@@ -213,20 +255,26 @@ int main(int argc, char** argv) {
   CK(hipStreamCreate(&st));
   if (mavg_fill_synthetic(x, n, dt, 0x5EED, 0, i16 ? 0 : dist, st) != MAVG_OK) return 1;
   size_t wsb = 0;
-  mavg_workspace_bytes(n, C, k, dt, MAVG_ALGO_BLELLOCH, 0, &wsb);
+  mavg_workspace_bytes(n, C, k, dt, algo, 0, &wsb);
   const size_t ws2 = std::max<size_t>(wsb, 256u << 20);  // also the r03 unit kernels' look-ahead records
   void* ws = nullptr;
   CK(hipMalloc(&ws, ws2));
   char plan[256];
-  mavg_plan(n, C, k, dt, MAVG_ALGO_BLELLOCH, 0, plan, sizeof plan);
+  mavg_plan(n, C, k, dt, algo, 0, plan, sizeof plan);
 
   const Sig sg{x, y, nullptr, n / C};
   std::vector<Var> vs;
   vs.push_back({std::string("lib: ") + plan, [=](hipStream_t s) {
-                  return mavg_run(x, y, n, C, k, dt, MAVG_ALGO_BLELLOCH, 0, nullptr, ws, wsb, s);
+                  return mavg_run(x, y, n, C, k, dt, algo, 0, nullptr, ws, wsb, s);
                 }, {}});
   vs.push_back({"copy", [=](hipStream_t s) { return mavg_stream_copy(x, y, n * eb, s); }, {}});
   const Workspace w2{ws, ws2};
+  if (hs) {
+    if (C == 1 && !i16) add_hs<float, double, 1>(vs, sg, k, w2);
+    else if (C == 2 && i16) add_hs<int16_t, int32_t, 2>(vs, sg, k, w2);
+    else if (C == 1 && i16) add_hs<int16_t, int32_t, 1>(vs, sg, k, w2);
+    else { fprintf(stderr, "hs: f32 mono, i16 mono or stereo\n"); return 1; }
+  } else
   switch (C * (i16 ? -1 : 1)) {
     case 1: add_wide<1>(vs, sg, k, w2); break;
     case 2: add_wide<2>(vs, sg, k, w2); break;
@@ -238,6 +286,9 @@ int main(int argc, char** argv) {
     case -8: add_wide_i16<8>(vs, sg, k, w2); break;
     default: fprintf(stderr, "C must be 1, 2, 4 or 8\n"); return 1;
   }
+  // the library's launch once more, last in the list (the first entry's position in the interleaved
+  // order is not neutral: it follows the copy in every forward round)
+  vs.push_back({"lib (last)", vs[0].run, {}});
   // reference output: the library
   if (vs[0].run(st) != MAVG_OK) return 1;
   CK(hipMemcpyAsync(yref, y, n * eb, hipMemcpyDeviceToDevice, st));
