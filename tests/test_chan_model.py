@@ -13,53 +13,65 @@ from test_lds_layout import chan_slot
 
 
 def chan_tile_model(x, k, C, Q, WG):
+    """eb = x's sample size: 4 (fp32, a lane owns one channel) or 2 (int16, a lane owns a dword
+    column of two channels, E = 2 accumulators, exact integer sums and truncating division)."""
+    eb = x.dtype.itemsize
+    E = 4 // eb                      # channels per dword column
+    CL = C // E                      # dword columns per frame
     nframes = len(x) // C
-    NW, NB, GPF = WG // 64, 64 // C, C // 4
-    WF, EPG = NB * Q, 4
+    NW, NB, GPF = WG // 64, 64 // CL, CL // 4
+    WF, EPG = NB * Q, 16 // eb
     TF = NW * WF
     TG = TF * GPF
     Hg = ((k * C + EPG - 1) // EPG + 15) // 16 * 16
     Hf = Hg * EPG // C
-    xs = x.reshape(-1, C).astype(np.float64)
-    out = np.zeros_like(xs)
+    acc = np.float64 if eb == 4 else np.int64
+    xs = x.reshape(-1, C).astype(acc)
+    out = np.zeros(xs.shape, dtype=np.float64 if eb == 4 else np.int16)
     lanes = np.arange(64)
-    c_of, b_of = lanes % C, lanes // C
+    col_of, b_of = lanes % CL, lanes // CL
     for tile in range((nframes + TF - 1) // TF):
         t0, h0 = tile * TF, tile * TF - Hf
-        stage = np.zeros((Hg + TG) * EPG)
+        stage = np.zeros((Hg + TG) * EPG, dtype=acc)
         e = np.arange((Hg + TG) * EPG)
         f, c = h0 + e // C, e % C
         ok = (f >= 0) & (f < nframes)
-        vals = np.where(ok, xs[np.clip(f, 0, nframes - 1), c], 0.0)
-        slots = np.array([chan_slot(g, C, Q) for g in range(Hg + TG)])
+        vals = np.where(ok, xs[np.clip(f, 0, nframes - 1), c], 0)
+        slots = np.array([chan_slot(g, CL, Q) for g in range(Hg + TG)])
         stage[slots[e // EPG] * EPG + e % EPG] = vals  # logical granule g lives in slot chan_slot(g)
 
-        def elem(ei):
-            return stage[slots[ei >> 2] * 4 + (ei & 3)]
+        def elem(ei):  # stage sample ei (frame * C + channel)
+            return stage[slots[ei // EPG] * EPG + ei % EPG]
 
-        W = np.zeros(C)
+        W = np.zeros(C, dtype=acc)
         for ei in range((Hf - k) * C, Hf * C):
             W[ei % C] += elem(ei)
-        run = np.zeros((NW, 64))
-        for w in range(NW):
-            f0 = Hf + w * WF + b_of * Q
-            for i in range(Q):
-                run[w] += elem((f0 + i) * C + c_of) - elem((f0 + i - k) * C + c_of)
-        incl, s = run.copy(), C
-        while s < 64:  # whole-wave shifts: lane l takes lane l - s
-            t = np.zeros_like(incl)
-            t[:, s:] = incl[:, :-s]
-            incl += t
-            s <<= 1
-        tot = incl[:, 64 - C:]  # [wave][channel]: the last block's lanes
-        for w in range(NW):
-            base = W[c_of] + sum(tot[i, c_of] for i in range(w)) + incl[w] - run[w]
-            f0 = Hf + w * WF + b_of * Q
-            for i in range(Q):
-                base = base + elem((f0 + i) * C + c_of) - elem((f0 + i - k) * C + c_of)
-                fr = t0 + w * WF + b_of * Q + i
-                m = fr < nframes
-                out[fr[m], c_of[m]] = base[m] / k
+        for ee in range(E):
+            ch = col_of * E + ee           # the channel each lane accumulates
+            run = np.zeros((NW, 64), dtype=acc)
+            for w in range(NW):
+                f0 = Hf + w * WF + b_of * Q
+                for i in range(Q):
+                    run[w] += elem((f0 + i) * C + ch) - elem((f0 + i - k) * C + ch)
+            incl, s = run.copy(), CL
+            while s < 64:  # whole-wave shifts: lane l takes lane l - s
+                t = np.zeros_like(incl)
+                t[:, s:] = incl[:, :-s]
+                incl += t
+                s <<= 1
+            tot = incl[:, 64 - CL:]  # [wave][column]: the last block's lanes
+            for w in range(NW):
+                base = W[ch] + sum(tot[i, col_of] for i in range(w)) + incl[w] - run[w]
+                f0 = Hf + w * WF + b_of * Q
+                for i in range(Q):
+                    base = base + elem((f0 + i) * C + ch) - elem((f0 + i - k) * C + ch)
+                    fr = t0 + w * WF + b_of * Q + i
+                    m = fr < nframes
+                    if eb == 4:
+                        out[fr[m], ch[m]] = base[m] / k
+                    else:  # C++ truncating division
+                        q = np.abs(base[m]) // k
+                        out[fr[m], ch[m]] = np.where(base[m] < 0, -q, q)
     return out.reshape(-1)
 
 
@@ -71,6 +83,34 @@ def test_chan_tile_model_equals_the_oracle(oracle_mod, C, Q, WG, k):
     got = chan_tile_model(x, k, C, Q, WG)
     ref = oracle_mod.mavg_f32(x, k, C).astype(np.float64)
     assert np.allclose(got, ref, rtol=1e-6, atol=1e-6), np.abs(got - ref).max()
+
+
+@pytest.mark.parametrize("Q,WG,k", [(32, 256, 2048), (32, 256, 3000), (16, 256, 1024), (16, 128, 77)])
+def test_chan_tile_model_int16_dword_columns(oracle_mod, Q, WG, k):
+    """int16 with 8 channels: a lane owns a dword column (two channels), the fp32 C = 4
+    addressing, bit-exact with the oracle."""
+    C = 8
+    frames = 16 * Q * (WG // 64) * 3 + 77
+    x = oracle_mod.synth_i16(frames * C, seed=k)
+    assert np.array_equal(chan_tile_model(x, k, C, Q, WG), oracle_mod.mavg_i16(x, k, C))
+
+
+@pytest.mark.parametrize("CL,P", [(8, 32), (4, 32), (4, 16)])
+def test_wide_ahead_offset_table_is_chan_slot(CL, P):
+    """wide_ahead_kernel's CH addressing (ch_table / ch_idx): element (frame j0 + i, column cl) of a
+    chan_slot stage at float index tb[i mod NBX] + (i / NBX) NBX 4 GPF, tb[r] = lb + (r ^ bq) 4 GPF --
+    the same index as chan_slot for every lane, wave and frame of the lane's block."""
+    NB, GPF = 64 // CL, CL // 4
+    NBX = min(NB, P)
+    for w in range(4):
+        for lane in range(64):
+            cl, bq = lane % CL, lane // CL
+            j0 = w * NB * P + bq * P
+            lb = (j0 * GPF + (cl >> 2)) * 4 + (cl & 3)
+            tb = [lb + (r ^ bq) * 4 * GPF for r in range(NBX)]
+            for i in range(P):
+                d = (j0 + i) * CL + cl
+                assert tb[i % NBX] + (i // NBX) * NBX * 4 * GPF == chan_slot(d >> 2, CL, P) * 4 + (d & 3)
 
 
 def test_row_local_shifts_would_be_wrong(oracle_mod):

@@ -58,22 +58,25 @@ void add_unit(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   vs.push_back({name, [=](hipStream_t s) { return dispatch_scan_f<T, A, C, F, false>(sg, k, 0, s, ws); }, {}});
 }
 
-template <typename T, typename A, int C, int P, int UW, int WG, int F, int U, int DV = 0>
+template <typename T, typename A, int C, int P, int UW, int WG, int F, int U, int DV = 0, bool XG = false>
 void addA(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D = 1024) {
   constexpr int kNtA = kNtStore | kNtHalo;
   char name[80];
-  snprintf(name, sizeof name, "wahead P%d U%d %d F%d U%d D%d dv%d", P, UW, WG, F, U, D, DV);
-  vs.push_back({name, [=](hipStream_t s) { return launch_wide_ahead<T, A, C, P, UW, WG, kNtA, DV, F, U>(sg, k, s, ws, D); }, {}});
+  snprintf(name, sizeof name, "wahead P%d U%d %d F%d U%d D%d dv%d xg%d", P, UW, WG, F, U, D, DV, (int)XG);
+  vs.push_back({name, [=](hipStream_t s) {
+                  return launch_wide_ahead<T, A, C, P, UW, WG, kNtA, DV, F, U, false, XG>(sg, k, s, ws, D);
+                }, {}});
 }
 
 // the look-ahead scan with U units per lane (tile = U * WG * F frames), as dispatched otherwise
 template <typename T, typename A, int C, int F, int U, bool RC, bool WREC, bool RUNS>
-void addU(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
+void addU(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D, size_t lds_floor = 0) {
   constexpr int kNtA = kNtStore | kNtHalo;
   char name[80];
-  snprintf(name, sizeof name, "ahead U%d wrec=%d runs=%d D%d", U, (int)WREC, (int)RUNS, D);
+  snprintf(name, sizeof name, "ahead U%d wrec=%d runs=%d D%d lds>=%zu", U, (int)WREC, (int)RUNS, D, lds_floor);
   vs.push_back({name, [=](hipStream_t s) {
-                  return launch_ahead_scan<T, A, C, F, U, kNtA, RC, true, WREC, 0, false, RUNS, 256>(sg, k, s, ws, D);
+                  return launch_ahead_scan<T, A, C, F, U, kNtA, RC, true, WREC, 0, false, RUNS, 256>(sg, k, s, ws, D,
+                                                                                                   false, lds_floor);
                 }, {}});
 }
 
@@ -120,9 +123,10 @@ void add_wide(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     if (k > 384 * 4096) addU<T, A, C, 4, 4, true, false, true>(vs, sg, k, ws, 1024);
     else if (k > 63 * 4096) addU<T, A, C, 4, 4, true, false, false>(vs, sg, k, ws, 1024);
     else addU<T, A, C, 4, 4, true, true, false>(vs, sg, k, ws, 512);
-    addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, 448);
-    addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, 384);
-    addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, 320);
+    // 8192-frame tiles (the dispatch past the L2 reach): the look-ahead distance, and a footprint
+    // cap through the LDS allocation (2 workgroups per CU instead of 3)
+    for (int D : {128, 192, 256, 320, 384}) addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, D);
+    for (int D : {160, 256, 320}) addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, D, 56 * 1024);
   } else {
     add_wide_c<C>(vs, sg, k, ws);
   }
@@ -135,9 +139,12 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   if (k > 1024) {  // the look-ahead range: the unit look-ahead against the wide look-ahead shapes
     add_unit<T, A, C, C == 2 ? 2 : 1>(vs, sg, k, ws);
     if constexpr (C == 2) {
-      addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws);
-      addA<T, A, C, 16, 1, 256, 2, 8>(vs, sg, k, ws);
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 512);
+      // the halo-only chunk form (x chunks straight from global memory, outputs through the shifted stage)
+      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 384);
+      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 512);
+      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 768);
+      addA<T, A, C, 16, 1, 256, 2, 8, 0, true>(vs, sg, k, ws, 512);
     } else if constexpr (C == 4) {
       addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws, 512);
       // the halo-only (XG) channel-per-lane look-ahead
@@ -146,7 +153,11 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
       addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 768);
       addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 1024);
       addAC<T, A, C, 16, 256, 1, 4, true, 5>(vs, sg, k, ws, 1024);
+      addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 384);
       addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 768);
+      addAC<T, A, C, 32, 128, 1, 8, true>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 32, 128, 1, 8, true>(vs, sg, k, ws, 1024);
     } else {
       addAC<T, A, C, 32, 256, 1, 4>(vs, sg, k, ws, 512);
       // the halo-only (XG) channel-per-lane look-ahead
@@ -200,9 +211,12 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
       addU<T, A, C, 4, 8, false, true, false>(vs, sg, k, ws, 192);
       addU<T, A, C, 4, 8, false, true, false>(vs, sg, k, ws, 128);
     } else if constexpr (C == 4) {
-      addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 1024);
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 512);
-      addA<T, A, C, 16, 1, 256, 4, 4>(vs, sg, k, ws, 512);
+      // the halo-only chunk form
+      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 384);
+      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 512);
+      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 768);
+      addA<T, A, C, 16, 1, 256, 4, 4, 0, true>(vs, sg, k, ws, 512);
     } else {
       addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws, 1024);
       // the halo-only channel-per-lane look-ahead with a dword column (2 channels) per lane
