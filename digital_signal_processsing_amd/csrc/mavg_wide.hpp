@@ -666,6 +666,10 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   constexpr int CE = CH ? 4 * C : P * C;   // (CH: unused)
   constexpr int G = CE / EPG;
   static_assert(CE % EPG == 0 && (G == 4 || G == 8), "64-B or 128-B chunks");
+  // XG: the halo-only form, CH only (the chunk form with x chunks from global memory and outputs
+  // through the shifted stage measured a tie, round 5: fp32 stereo k=44100 0.639 -> 0.645, int16 4
+  // channels 0.615 -> 0.613; profiles/r05_tuning/wide/chunkxg_*)
+  static_assert(!XG || CH, "the halo-only form is the channel-per-lane form's");
   using CEl = ChanElem<T>;                 // CH: a stage dword as E samples (fp32 1, int16 2)
   constexpr int E = CEl::E;
   constexpr int CL = C / E > 0 ? C / E : 1;  // CH: dword columns per frame (a lane owns one)
@@ -749,38 +753,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   // first barrier, or after the record carry with the in-tile scan moved there -- 118 instead of 150
   // VGPRs for 8 channels -- both slower: C = 8, k = 44100 0.570 -> 0.518 / 0.487; the tile's x
   // latency then lies on the tile's path)
-  if constexpr (XG && CH) load_x();
-  // XG without CH (chunks): the lane's UW chunks of x, 16-B loads straight from global memory
-  constexpr int NWDc = (CE / EPG) * 4;  // dwords per chunk
-  uint32_t xc[XG && !CH ? UW : 1][XG && !CH ? NWDc : 1];
-  if constexpr (XG && !CH) {
-#pragma unroll
-    for (int uw = 0; uw < UW; ++uw) {
-      const long long f = t0 + (long long)(uw * WG + tid) * P;
-      if (tile_full) {
-        const u32x4* src = reinterpret_cast<const u32x4*>(in + f * C);
-#pragma unroll
-        for (int i = 0; i < NWDc / 4; ++i) {
-          const u32x4 v = src[i];
-          xc[uw][4 * i] = v[0];
-          xc[uw][4 * i + 1] = v[1];
-          xc[uw][4 * i + 2] = v[2];
-          xc[uw][4 * i + 3] = v[3];
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < NWDc * (int)(4 / sizeof(T)); ++i) {
-          const T v = load_elem(in, hist, f + i / C, i % C, C, nframes, k, pre);
-          if constexpr (sizeof(T) == 4) {
-            xc[uw][i] = __float_as_uint(v);
-          } else {
-            const uint32_t h = (uint32_t)(uint16_t)v << (16 * (i & 1));
-            xc[uw][i >> 1] = (i & 1) ? (xc[uw][i >> 1] | h) : h;
-          }
-        }
-      }
-    }
-  }
+  if constexpr (XG) load_x();
   // phase A's tile (its loads issued after the stage: issued first they measured 0.581 -> 0.534 for
   // 8 channels at k = 44100, profiles/r05_tuning/wide/pa_*)
   Unit<T, VE> xa[U];
@@ -873,18 +846,6 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
 #pragma unroll
     for (int h = 0; h < NG; ++h) rv[h] = 0ull;
   }
-  // the second round's granules too (8 channels at k = 44100: 344 slots), so the carry does not wait
-  // for a second L2 round trip after the first round
-#ifndef MAVG_WIDE_PRELOAD2
-#define MAVG_WIDE_PRELOAD2 1
-#endif
-  unsigned long long rv2[NG];
-  if (MAVG_WIDE_PRELOAD2 && tid + WG < nslot) {
-    slot_load(tid + WG, rv2);
-  } else {
-#pragma unroll
-    for (int h = 0; h < NG; ++h) rv2[h] = 0ull;
-  }
   __syncthreads();
   // the three record sources (phase A, own tile, head duty), one per wave: a
   // loop, so a 2-wave workgroup (128 threads) publishes its head-duty records too
@@ -926,16 +887,8 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
     d[3] = v[3];
   };
   auto x_chunk = [&](int j, uint32_t (&xv)[NWD]) {
-    if constexpr (XG && !CH) {  // from registers: chunk j = uw * WG + tid
 #pragma unroll
-      for (int uw = 0; uw < UW; ++uw)
-        if (j == uw * WG + tid)
-#pragma unroll
-          for (int i = 0; i < NWD; ++i) xv[i] = xc[uw][i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < G; ++i) gwords(tstage, j * G + i, xv + 4 * i);
-    }
+    for (int i = 0; i < G; ++i) gwords(tstage, j * G + i, xv + 4 * i);
   };
   auto xk_chunk = [&](int j, uint32_t (&xk)[NWD]) {
     const int e = (Ha - k) * C + j * CE;  // shifted-stage element of x[n-k] for the chunk's first frame
@@ -1056,10 +1009,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   for (long long sb0 = 0; sb0 < nslot; sb0 += WG) {
     const long long sl = sb0 + tid;
     const bool act = sl < nslot;
-    if (MAVG_WIDE_PRELOAD2 && sb0 == WG) {
-#pragma unroll
-      for (int h = 0; h < NG; ++h) rv[h] = rv2[h];
-    } else if (sb0 != 0) {
+    if (sb0 != 0) {
       if (act) {
         slot_load(sl, rv);
       } else {
@@ -1244,7 +1194,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   __syncthreads();  // every read of the tile stage is done: it takes the outputs
 #pragma unroll
   for (int uw = 0; uw < UW; ++uw) {
-    unsigned char* rb = (XG ? sstage : tstage) + ((uw * WG + wq * 64) * G) * 16;  // XG: the shifted stage
+    unsigned char* rb = tstage + ((uw * WG + wq * 64) * G) * 16;
 #pragma unroll
     for (int i = 0; i < G; ++i) {
       Gr g;
@@ -1258,7 +1208,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
   for (int uw = 0; uw < UW; ++uw) {
-    const unsigned char* rb = (XG ? sstage : tstage) + ((uw * WG + wq * 64) * G) * 16;
+    const unsigned char* rb = tstage + ((uw * WG + wq * 64) * G) * 16;
     T* ob = out + (t0 + (long long)(uw * WG + wq * 64) * P) * C;
 #pragma unroll
     for (int r = 0; r < G; ++r) {

@@ -139,12 +139,9 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   if (k > 1024) {  // the look-ahead range: the unit look-ahead against the wide look-ahead shapes
     add_unit<T, A, C, C == 2 ? 2 : 1>(vs, sg, k, ws);
     if constexpr (C == 2) {
+      addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 384);
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 512);
-      // the halo-only chunk form (x chunks straight from global memory, outputs through the shifted stage)
-      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 384);
-      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 512);
-      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 768);
-      addA<T, A, C, 16, 1, 256, 2, 8, 0, true>(vs, sg, k, ws, 512);
+      addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 768);
     } else if constexpr (C == 4) {
       addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws, 512);
       // the halo-only (XG) channel-per-lane look-ahead
@@ -211,12 +208,9 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
       addU<T, A, C, 4, 8, false, true, false>(vs, sg, k, ws, 192);
       addU<T, A, C, 4, 8, false, true, false>(vs, sg, k, ws, 128);
     } else if constexpr (C == 4) {
+      addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 384);
       addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 512);
-      // the halo-only chunk form
-      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 384);
-      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 512);
-      addA<T, A, C, 8, 1, 256, 2, 4, 0, true>(vs, sg, k, ws, 768);
-      addA<T, A, C, 16, 1, 256, 4, 4, 0, true>(vs, sg, k, ws, 512);
+      addA<T, A, C, 8, 1, 256, 2, 4>(vs, sg, k, ws, 768);
     } else {
       addA<T, A, C, 4, 1, 256, 1, 4>(vs, sg, k, ws, 1024);
       // the halo-only channel-per-lane look-ahead with a dword column (2 channels) per lane
