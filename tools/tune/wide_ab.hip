@@ -297,6 +297,25 @@ int main(int argc, char** argv) {
   // the library's launch once more, last in the list (the first entry's position in the interleaved
   // order is not neutral: it follows the copy in every forward round)
   vs.push_back({"lib (last)", vs[0].run, {}});
+  // WIDE_AB_LIST: the variants' indices; WIDE_AB_ONLY=<i>: variant i alone, 1 + 10 launches and no
+  // check -- every dispatch of such a run apart from the input fill and the workspace memsets is
+  // variant i's, so one rocprofv3 --pmc pass measures that variant (tools/gpu/r05_footprint_pmc.sh)
+  if (getenv("WIDE_AB_LIST")) {
+    for (size_t v = 0; v < vs.size(); ++v) printf("%zu\t%s\n", v, vs[v].name.c_str());
+    return 0;
+  }
+  if (const char* only = getenv("WIDE_AB_ONLY")) {
+    const int vi = atoi(only);
+    if (vi < 0 || vi >= (int)vs.size()) {
+      fprintf(stderr, "WIDE_AB_ONLY=%d: %zu variants\n", vi, vs.size());
+      return 1;
+    }
+    for (int i = 0; i < 1 + steps; ++i)
+      if (vs[vi].run(st) != MAVG_OK) return 1;
+    CK(hipStreamSynchronize(st));
+    printf("%d\t%s\n", vi, vs[vi].name.c_str());
+    return 0;
+  }
   // reference output: the library
   if (vs[0].run(st) != MAVG_OK) return 1;
   CK(hipMemcpyAsync(yref, y, n * eb, hipMemcpyDeviceToDevice, st));
