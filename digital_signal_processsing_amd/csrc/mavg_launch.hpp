@@ -488,7 +488,12 @@ int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   const long long ntiles = (nframes + TF - 1) / TF;
   const long long nfull = nframes / TF;
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
-  const size_t need = ahead_granule_bytes<T, A, C, F, U>(nfull);  // per-tile records + 16
+#ifdef MAVG_AHEAD_TRACE
+  const size_t trace_bytes = (size_t)ntiles * 64;  // tuning builds: 8 stamps per tile, after the stats
+#else
+  const size_t trace_bytes = 0;
+#endif
+  const size_t need = ahead_granule_bytes<T, A, C, F, U>(nfull) + trace_bytes;  // per-tile records + 16
   // the shifted tile (+ one granule for an x[n-k] extraction) and, unless XG, the tile
   const size_t lds = (size_t)((XG ? 1 : 2) * TG + 1) * 16 + (size_t)NW * C * sizeof(A) +
                      (size_t)(NSEG + 3 * NW) * C * sizeof(SA);
@@ -525,7 +530,10 @@ int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.self = 0;
   p.gran = static_cast<unsigned long long*>(ws.ptr);
   p.runs = nullptr;
-  p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
+  p.stats = static_cast<unsigned char*>(ws.ptr) + need - trace_bytes - 16;
+#ifdef MAVG_AHEAD_TRACE
+  p.trace = reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(ws.ptr) + need - trace_bytes);
+#endif
   if (lds > 64 * 1024) {
     const int s = raise_dyn_lds_limit<&wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH, XG, MW>>(80 * 1024);
     if (s != MAVG_OK) return s;

@@ -718,6 +718,10 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   const long long a = t0 - k;
   const long long jlo = a >= 0 ? (a + TF - 1) / TF : 0;
   const long long qlo = jlo, qhi = tile;  // per-tile records of the whole tiles [jlo, tile)
+  // MAVG_AHEAD_TRACE (tuning builds, tools/tune/ahead_trace.py): thread 0's phase stamps, the
+  // mono look-ahead's slots: 0 start, 1 phase A summed, 2 first barrier, 3 in-tile scan, 4 wave
+  // 0's carry items, 5 second barrier, 6 outputs issued, 7 wave 0's polls
+  if (tid == 0) MAVG_ATRACE(0, MAVG_ANOW());
   const int pcount = a >= 0 ? (int)(jlo * TF - a) : 0;
   const long long nitem = qhi - qlo;
 
@@ -810,6 +814,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
     wave_record<T, SA, C, F, U>(xa, r);
     share(0, r);
   }
+  if (tid == 0) MAVG_ATRACE(1, MAVG_ANOW());
   const bool own = blockIdx.x < (unsigned)p.ahead && tile < p.nfull;  // no block D slots earlier
   if (own) {
     SA r[C];
@@ -847,6 +852,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
     for (int h = 0; h < NG; ++h) rv[h] = 0ull;
   }
   __syncthreads();
+  if (tid == 0) MAVG_ATRACE(2, MAVG_ANOW());
   // the three record sources (phase A, own tile, head duty), one per wave: a
   // loop, so a 2-wave workgroup (128 threads) publishes its head-duty records too
   for (int src = wq; src < 3; src += NW) {
@@ -1003,8 +1009,12 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
     }
   }
 
+  if (tid == 0) MAVG_ATRACE(3, MAVG_ANOW());
   // ---- 4. whole-tile carry from the records, WG (record, channel) slots per round ----
   A hq = (A)0;  // channel cc
+#ifdef MAVG_AHEAD_TRACE
+  unsigned polls0 = 0;
+#endif
 #pragma unroll 1
   for (long long sb0 = 0; sb0 < nslot; sb0 += WG) {
     const long long sl = sb0 + tid;
@@ -1024,6 +1034,9 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
     for (int it = 0; __any(miss) && it < p.spin; ++it) {
 #ifdef MAVG_AHEAD_STATS
       if (lane == 0) atomicAdd(reinterpret_cast<unsigned int*>(p.stats) + 1, 1u);
+#endif
+#ifdef MAVG_AHEAD_TRACE
+      ++polls0;
 #endif
       __builtin_amdgcn_s_sleep(2);
       if (miss) slot_load(sl, rv);
@@ -1063,20 +1076,50 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
       hq += (A)gran_value<SA>(wd);
     }
   }
+  if (tid == 0) {
+    MAVG_ATRACE(4, MAVG_ANOW());
+#ifdef MAVG_AHEAD_TRACE
+    MAVG_ATRACE(7, polls0);
+#endif
+  }
+  if constexpr (CH) {
+    // the wave's per-channel totals by butterflies over the lanes of one channel (lane mod C
+    // for the carry and the history, lane mod CL for the partial window's column sums)
+    // instead of C whole-wave scans: at C = 8 the scans took 1.5 us of an 11.4-us tile
+    // (the phase trace, profiles/r05_tuning/trace/)
+    static_assert(64 % C == 0 && 64 % CL == 0 && CL * E == C, "channel = lane mod C; column = lane mod CL");
+    A v = hp[0] + hq;  // channel cc = lane mod C
+    if constexpr (E == 1) v += hpo[0];  // the column is the channel
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    A part;
-    if constexpr (CH) {
-      part = cc == c ? hp[0] + hq : (A)0;
+    for (int sh = C; sh < 64; sh <<= 1) v += __shfl_xor(v, sh, 64);
+    if constexpr (E > 1) {
+      A hv[E];
 #pragma unroll
-      for (int e = 0; e < E; ++e)
-        if (cl * E + e == c) part += hpo[e];
+      for (int e = 0; e < E; ++e) {
+        hv[e] = hpo[e];
+#pragma unroll
+        for (int sh = CL; sh < 64; sh <<= 1) hv[e] += __shfl_xor(hv[e], sh, 64);
+      }
+      // lane l < C takes channel l's column total from lane l / E (element l mod E)
+      A add = (A)0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const A t = __shfl(hv[e], lane / E, 64);
+        if (lane % E == e) add = t;
+      }
+      v += add;
     }
-    else part = hp[c] + (cc == c ? hq : (A)0);
-    const A r = readlane(wave_incl_scan(part), 63);
-    if (lane == 0) hsum[w * C + c] = r;
+    if (lane < C) hsum[w * C + lane] = v;
+  } else {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const A part = hp[c] + (cc == c ? hq : (A)0);
+      const A r = readlane(wave_incl_scan(part), 63);
+      if (lane == 0) hsum[w * C + c] = r;
+    }
   }
   __syncthreads();
+  if (tid == 0) MAVG_ATRACE(5, MAVG_ANOW());
 
   // ---- 5. carry + earlier segments; pass 2 rebuilt from the stages; outputs ----
   if constexpr (CH) {
@@ -1145,6 +1188,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
       const Gr g = GIO::load(reinterpret_cast<const T*>(sstage + s2 * 16));
       GIO::template store<(NT & kNtStore) != 0>(ob + (long long)(chan_slot<CL, P>(s2) - rg) * EPG, g);
     }
+    if (tid == 0) MAVG_ATRACE(6, MAVG_ANOW());
     return;
   }
   static_assert(NSEG <= 64, "segment totals are scanned across one wave");
@@ -1217,6 +1261,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
       GIO::template store<(NT & kNtStore) != 0>(ob + out_slot(s) * EPG, g);
     }
   }
+  if (tid == 0) MAVG_ATRACE(6, MAVG_ANOW());
 }
 
 }  // namespace mavg

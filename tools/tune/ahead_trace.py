@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--algo", type=int, default=0)
     ap.add_argument("--log2n", type=int, default=30)
     ap.add_argument("--launches", type=int, default=4)
+    ap.add_argument("--slots", default=None,
+                    help="an experiment build's stamp order, e.g. 0,2,4,1,5,3,6: consecutive differences only")
     a = ap.parse_args()
     n = 1 << a.log2n
     tdt = torch.float32 if a.dtype == "f32" else torch.int16
@@ -46,7 +48,7 @@ def main():
     buf = ctypes.create_string_buffer(512)
     assert lib.mavg_plan(n, a.c, a.k, code, a.algo, 0, buf, 512) == 0
     plan = buf.value.decode()
-    assert plan.startswith("ahead_scan<"), plan
+    assert plan.startswith(("ahead_scan<", "wide_ahead<")), plan
     ntiles = int(re.search(r"grid=(\d+)", plan).group(1))
     plan_ws = int(re.search(r"ws=(\d+)", plan).group(1))  # this launch's need: the trace ends there
     need = ctypes.c_size_t(0)
@@ -74,6 +76,13 @@ def main():
     st = (tr[:, :7] - t0) * 10  # ns
     span = (st[:, 6].max() - st[:, 0].min()) / 1e3
     print(f"tiles {ntiles}, traced span {span:.1f} us")
+    if a.slots:
+        order = [int(v) for v in a.slots.split(",")]
+        for i, j in zip(order, order[1:]):
+            d = (st[:, j] - st[:, i]) / 1e3
+            print(f"  stamp {i} -> {j}: median {np.median(d):7.2f} us  mean {d.mean():7.2f}  p10 {np.percentile(d, 10):7.2f}  "
+                  f"p90 {np.percentile(d, 90):7.2f}")
+        return
     names = ["phase A (start->1)", "to first barrier (1->2)", "publish + in-tile scan (2->3)",
              "carry items (3->4)", "second barrier (4->5)", "outputs issued (5->6)", "lifetime (start->end)"]
     pairs = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (0, 6)]
