@@ -730,10 +730,10 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     if (halo_bytes <= 32768) return launch_chan_tile<T, A, C, 32, kWG, kNtS>(sg, k, st);
     // past it: the halo-only look-ahead (XG: x straight from global memory, only the shifted tile in
     // LDS, 33 KiB instead of 65 KiB; round 5, in-process, profiles/r05_tuning/wide/pa0_c8_*: k=44100
-    // 0.429 -> 0.589 (D = 384), k=2048 0.534 (the halo-only tile) -> 0.616); up to 128 KiB of halo in
-    // 128-thread workgroups (512-frame tiles, D = 512: k=1536..4096 +0.5-1 %, wide_ab_f32_c8_k*.log;
-    // at k=44100 they lose, 0.589 -> 0.516)
-    if (halo_bytes <= 131072) return launch_wide_ahead<T, A, C, 32, 1, 128, kNtA, 0, 1, 4, true, true>(sg, k, st, ws, 512);
+    // 0.429 -> 0.589 (D = 384), k=2048 0.534 (the halo-only tile) -> 0.616).  256 threads at every
+    // such window: with the per-channel totals by butterflies the 128-thread form (512-frame tiles,
+    // once +0.5-1 % at k = 1536..4096) ties or loses (in-process, profiles/r05_tuning/wide/
+    // after_butterfly/: k=2048 0.672 vs 0.670 on one box, pass12_*: 0.700 vs 0.604 on another)
     return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 4, true, true>(sg, k, st, ws, 384);
   } else if constexpr (sizeof(T) == 2 && C == 4) {
     if constexpr (sizeof(A) == 4) {

@@ -3,6 +3,8 @@
 // consecutive frames per lane.
 #pragma once
 
+#include <type_traits>
+
 #include "mavg_device.hpp"
 #include "mavg_lookback.hpp"
 
@@ -943,9 +945,10 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   A hpo[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) crun[e] = cincl[e] = (SA)0, hpo[e] = (A)0;
-  auto ch_pass1 = [&]() {
-    static_assert(!CH || (F == 1 && NBX * (P / NBX) == P), "Ha = k: x[n-k] of tile frame f is shifted-stage frame f");
-    MAVG_DCHECK(Ha == k, "CH shifted stage offset", Ha, k);
+  // (PW: the wave holds frames of the partial window's x[n-k], frames < pcount -- wave-uniform,
+  // so the other waves run the loop without its per-frame select)
+  auto ch_pass1_loop = [&](auto pw) {
+    constexpr bool PW = decltype(pw)::value;
     int tb[NBX];
     ch_table(ch_lb, ch_bq, tb);
 #pragma unroll
@@ -960,10 +963,17 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
       else xv = tsf[ix];
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        if (j0 + i < pcount) hpo[e] += to_acc<A>(CEl::get(xk, e));
+        if constexpr (PW)
+          if (j0 + i < pcount) hpo[e] += to_acc<A>(CEl::get(xk, e));
         crun[e] += to_acc<SA>(CEl::get(xv, e)) - to_acc<SA>(CEl::get(xk, e));
       }
     }
+  };
+  auto ch_pass1 = [&]() {
+    static_assert(!CH || (F == 1 && NBX * (P / NBX) == P), "Ha = k: x[n-k] of tile frame f is shifted-stage frame f");
+    MAVG_DCHECK(Ha == k, "CH shifted stage offset", Ha, k);
+    if (pcount > wq * WF) ch_pass1_loop(std::true_type{});
+    else ch_pass1_loop(std::false_type{});
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       cincl[e] = crun[e];
@@ -1151,9 +1161,10 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
     // read of (the same lane, the same address: no barrier); the wave then
     // reads its own frames back slot-contiguous
     uint32_t* sw = reinterpret_cast<uint32_t*>(sstage);
-    SA run[E];
+    // the window sum itself runs through the frames (base folded in: one add per sample fewer)
+    A run[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) run[e] = (SA)0;
+    for (int e = 0; e < E; ++e) run[e] = base[e];
 #pragma unroll
     for (int i = 0; i < P; ++i) {
       if (i % kGrp == 0 && i > 0) __builtin_amdgcn_sched_barrier(0);
@@ -1165,8 +1176,8 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
       T y[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        run[e] += to_acc<SA>(CEl::get(xv, e)) - to_acc<SA>(CEl::get(xk, e));
-        y[e] = to_out<T, A, DV>(base[e] + (A)run[e], p.o);
+        run[e] += (A)(to_acc<SA>(CEl::get(xv, e)) - to_acc<SA>(CEl::get(xk, e)));
+        y[e] = to_out<T, A, DV>(run[e], p.o);
       }
       if (tile_full) {
         sw[ix] = CEl::put(y);
