@@ -523,14 +523,28 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
     }
     // element i of this thread's granules is channel (cb + i) mod C (granules WG apart: whole frames)
     const int cb = ((g0 + tid) * EPG) % C;
+    if constexpr (EPG < C && C % EPG == 0) {
+      // fp32 C = 8: cb repeats every C / EPG lanes (the lane's parity), and those lanes' elements
+      // are the C channels once each -- butterflies over the lanes of one residue instead of C
+      // whole-wave fp64 scans (in-process, profiles/r05_tuning/wide/cand_chanbf_*: k=1536 0.649 ->
+      // 0.663, k=1024 0.738 -> 0.740)
 #pragma unroll
-    for (int ch = 0; ch < C; ++ch) {
-      A part = (A)0;
+      for (int sh = C / EPG; sh < 64; sh <<= 1)
 #pragma unroll
-      for (int i = 0; i < EPG; ++i)
-        if ((cb + i) % C == ch) part += hs[i];
-      const A r = readlane(wave_incl_scan(part), 63);
-      if (lane == 0) hsum[w * C + ch] = r;
+        for (int i = 0; i < EPG; ++i) hs[i] += __shfl_xor(hs[i], sh, 64);
+      if (lane < C / EPG)
+#pragma unroll
+        for (int i = 0; i < EPG; ++i) hsum[w * C + (cb + i) % C] = hs[i];
+    } else {
+#pragma unroll
+      for (int ch = 0; ch < C; ++ch) {
+        A part = (A)0;
+#pragma unroll
+        for (int i = 0; i < EPG; ++i)
+          if ((cb + i) % C == ch) part += hs[i];
+        const A r = readlane(wave_incl_scan(part), 63);
+        if (lane == 0) hsum[w * C + ch] = r;
+      }
     }
   }
 
@@ -1121,6 +1135,8 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
     }
     if (lane < C) hsum[w * C + lane] = v;
   } else {
+    // (hp holds every channel in every thread -- the chunk scan of step 3 sums the partial
+    // window's x[n-k] into it -- so these stay whole-wave scans)
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const A part = hp[c] + (cc == c ? hq : (A)0);

@@ -52,6 +52,36 @@ def test_loaded_libraries_are_built_from_this_tree():
         assert _lib.build_id(path) == want, (path, "stale library: rebuild with __graft_entry__.build()")
 
 
+def _dynamic_flags(path):
+    """DT_FLAGS of an ELF64 little-endian shared object (0 when absent)."""
+    import struct
+    data = open(path, "rb").read()
+    assert data[:4] == b"\x7fELF" and data[4] == 2 and data[5] == 1, path
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", data, 0x3A)
+    for i in range(shnum):
+        sh_type, = struct.unpack_from("<I", data, shoff + i * shentsize + 4)
+        if sh_type != 6:  # SHT_DYNAMIC
+            continue
+        off, size = struct.unpack_from("<QQ", data, shoff + i * shentsize + 0x18)
+        flags = 0
+        for j in range(0, size, 16):
+            tag, val = struct.unpack_from("<qQ", data, off + j)
+            if tag == 30:  # DT_FLAGS
+                flags = val
+        return flags
+    return 0
+
+
+def test_library_binds_its_own_kernels():
+    """Every build is linked -Bsymbolic (DF_SYMBOLIC): a kernel template instance is a weak
+    symbol, and without it a program instantiating the same kernel from other sources (a tuner
+    built from an older tree) interposes its host stub, so the library's own launches would run
+    that program's code object (round 5: an in-process A/B that compared nothing)."""
+    for path in (_lib.LIB_PATH, _lib.DEBUG_LIB_PATH, _lib.HOOKS_LIB_PATH):
+        assert _dynamic_flags(path) & 0x2, path  # DF_SYMBOLIC
+
+
 def test_build_id_follows_the_sources(tmp_path):
     """The id changes with any byte of a source file, and only with the sources."""
     import shutil

@@ -155,6 +155,10 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
       addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 768);
       addAC<T, A, C, 32, 128, 1, 8, true>(vs, sg, k, ws, 512);
       addAC<T, A, C, 32, 128, 1, 8, true>(vs, sg, k, ws, 1024);
+      // 4 workgroups per CU (<= 128 VGPRs) instead of 3 (142)
+      addAC<T, A, C, 32, 256, 1, 8, true, 4>(vs, sg, k, ws, 384);
+      addAC<T, A, C, 32, 256, 1, 8, true, 4>(vs, sg, k, ws, 512);
+      addAC<T, A, C, 32, 256, 1, 8, true, 4>(vs, sg, k, ws, 768);
     } else {
       addAC<T, A, C, 32, 256, 1, 4>(vs, sg, k, ws, 512);
       // the halo-only (XG) channel-per-lane look-ahead
