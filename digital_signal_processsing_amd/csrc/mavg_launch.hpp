@@ -707,10 +707,12 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     if (k >= 2048 && halo_bytes <= 57344) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
     if (halo_bytes <= 4096) return launch_wide_tile<T, A, C, 8, 2, kWG, kNtS>(sg, k, st);
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
-    // past the halo-only tile: the halo-only channel-per-lane look-ahead, 2048-frame tiles (round 5,
-    // in-process, profiles/r05_tuning/wide/pa0_c4_k44100.log: k=44100 0.540 -> 0.593 against the
-    // chunk look-ahead)
-    return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 8, true, true>(sg, k, st, ws, 512);
+    // past the halo-only tile: the halo-only channel-per-lane look-ahead (round 5, in-process,
+    // profiles/r05_tuning/wide/pa0_c4_k44100.log: k=44100 0.540 -> 0.593 against the chunk
+    // look-ahead), in 1024-frame tiles (16 frames per lane, 92 VGPRs, D = 768) rather than 2048
+    // (142 VGPRs): 0.612 -> 0.622 and 0.612 -> 0.617 on two boxes (after_butterfly/ab_f32_c4_k44100,
+    // ab_f32_c4_k44100_mw4)
+    return launch_wide_ahead<T, A, C, 16, 1, kWG, kNtA, 0, 1, 4, true, true>(sg, k, st, ws, 768);
   } else if constexpr (sizeof(T) == 4 && C == 8) {
     // one channel per lane (chan_tile_kernel, 32 frames each): one scan per
     // tile row for all 8 channels instead of 8 per chunk (in-process A/B,

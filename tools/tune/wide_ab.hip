@@ -94,13 +94,13 @@ void addAC(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
 // the Hillis-Steele look-ahead (mono / stereo) at several look-ahead distances; per-wave records
 // for mono as dispatched.  (Round 5 also measured the log-step scans rebuilt after the carry, RC:
 // fewer registers, slower -- profiles/r05_tuning/hs/; the kernel no longer has that form.)
-template <typename T, typename A, int C, int F, bool WREC>
+template <typename T, typename A, int C, int F, bool WREC, int U = 4>
 void addH(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
   constexpr int kNtA = kNtStore | kNtHalo;
   char name[80];
-  snprintf(name, sizeof name, "hillis ahead wrec=%d D%d", (int)WREC, D);
+  snprintf(name, sizeof name, "hillis ahead U%d wrec=%d D%d", U, (int)WREC, D);
   vs.push_back({name, [=](hipStream_t s) {
-                  return launch_ahead_scan<T, A, C, F, 4, kNtA, false, true, WREC, 0, true, false, 256>(sg, k, s, ws, D);
+                  return launch_ahead_scan<T, A, C, F, U, kNtA, false, true, WREC, 0, true, false, 256>(sg, k, s, ws, D);
                 }, {}});
 }
 template <typename T, typename A, int C>
@@ -109,6 +109,11 @@ void add_hs(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   for (int D : {384, 512, 768}) {
     if constexpr (C == 1) addH<T, A, C, F, true>(vs, sg, k, ws, D);
     else addH<T, A, C, F, false>(vs, sg, k, ws, D);
+  }
+  // half tiles: 76-82 VGPRs (fp32) instead of 120-126, 6 waves per SIMD instead of 4
+  for (int D : {512, 768, 1024, 1536}) {
+    addH<T, A, C, F, true, 2>(vs, sg, k, ws, D);
+    addH<T, A, C, F, false, 2>(vs, sg, k, ws, D);
   }
 }
 
