@@ -242,6 +242,10 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   } else if constexpr (C == 8) {
     add1<T, A, C, 8, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 4, 2, 256, 0>(vs, sg, k);
+    // the halo-only channel-per-lane look-ahead (82 VGPRs) at tile-scan windows too
+    addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 384);
+    addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 512);
+    addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 384);
     // the channel-per-lane tile with two channels (a dword column) per lane
     addC<T, A, C, 32, 256>(vs, sg, k);
     addC<T, A, C, 16, 256>(vs, sg, k);
