@@ -132,6 +132,8 @@ void add_wide(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     // cap through the LDS allocation (2 workgroups per CU instead of 3)
     for (int D : {128, 192, 256, 320, 384}) addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, D);
     for (int D : {160, 256, 320}) addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, D, 56 * 1024);
+    // 4096-frame tiles (84-90 VGPRs, 5 waves per SIMD) against the 8192-frame ones (142, 3)
+    for (int D : {384, 512, 640, 768}) addU<T, A, C, 4, 4, true, false, false>(vs, sg, k, ws, D);
   } else {
     add_wide_c<C>(vs, sg, k, ws);
   }
