@@ -192,7 +192,11 @@ int launch_wide_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
 
 // the channel-per-lane tile (mavg_wide.hpp chan_tile_kernel): lanes own one
 // channel of Q frames; same stage, halo and workspace-free launch as the wide tile
-template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false>
+// IPOK: with XG and a staged halo of exactly k frames (k C elements fill whole 256-B rows), the
+// in-place output form (chan_tile_kernel IP).  In-process (profiles/r05_tuning/wide/ip_*): fp32
+// C = 4 k=2048 0.737 -> 0.756; fp32 C = 8 k=1024 0.750 -> 0.746 and int16 C = 8 k=2048 0.649 ->
+// 0.485 (170 VGPRs, 2 workgroups per CU), so only fp32 C = 4 asks for it
+template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false, bool IPOK = false>
 int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
   constexpr int EPG = 16 / (int)sizeof(T);
   constexpr int NW = WG / 64;
@@ -207,10 +211,12 @@ int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
   if (lds > 80 * 1024) return MAVG_ERR_UNSUPPORTED;
   const long long ntiles = (nframes + TF - 1) / TF;
   if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  const bool ip = XG && IPOK && Hg * EPG == (long long)k * C;  // staged halo frames Hg EPG / C == k
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "chan_tile<%s,acc=%s,C=%d,Q=%d,nt=%d,dv=%d%s> grid=%lld block=%d lds=%zu tile_frames=%d remap=%d",
-             type_name<T>(), type_name<A>(), C, Q, NT, DV, XG ? ",xg=1" : "", ntiles, WG, lds, TF, xcd_remap);
+             "chan_tile<%s,acc=%s,C=%d,Q=%d,nt=%d,dv=%d%s%s> grid=%lld block=%d lds=%zu tile_frames=%d remap=%d",
+             type_name<T>(), type_name<A>(), C, Q, NT, DV, XG ? ",xg=1" : "", ip ? ",ip=1" : "", ntiles, WG, lds, TF,
+             xcd_remap);
     return MAVG_OK;
   }
   WideParams p{};
@@ -225,12 +231,19 @@ int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
   p.xcd_remap = xcd_remap;
   p.pre = sg.pre;
   p.o = make_out_params(k);
-  if (lds > 64 * 1024) {
-    const int s = raise_dyn_lds_limit<&chan_tile_kernel<T, A, C, Q, WG, NT, DV, XG>>(80 * 1024);
-    if (s != MAVG_OK) return s;
+  auto launch = [&](auto ipc) -> int {
+    constexpr bool IP = decltype(ipc)::value;
+    if (lds > 64 * 1024) {
+      const int s = raise_dyn_lds_limit<&chan_tile_kernel<T, A, C, Q, WG, NT, DV, XG, IP>>(80 * 1024);
+      if (s != MAVG_OK) return s;
+    }
+    hipLaunchKernelGGL((chan_tile_kernel<T, A, C, Q, WG, NT, DV, XG, IP>), dim3((unsigned)ntiles), dim3(WG), lds, st, p);
+    return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+  };
+  if constexpr (XG && IPOK) {
+    if (ip) return launch(std::true_type{});
   }
-  hipLaunchKernelGGL((chan_tile_kernel<T, A, C, Q, WG, NT, DV, XG>), dim3((unsigned)ntiles), dim3(WG), lds, st, p);
-  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+  return launch(std::false_type{});
 }
 
 // look-ahead scan (one pass over HBM): zero the record granules, then one
@@ -704,7 +717,7 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     // 2048 <= k <= 3584: the halo-only channel-per-lane tile (2048-frame tiles; in-process,
     // profiles/r04_tuning/chan/xg_c4_*, xgr_*: k=2048 0.660 -> 0.712 against the wide tile, 3000
     // 0.541 -> 0.675 against the wide look-ahead; k=4096 ties it, 0.559 vs 0.556)
-    if (k >= 2048 && halo_bytes <= 57344) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
+    if (k >= 2048 && halo_bytes <= 57344) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true, true>(sg, k, st);
     if (halo_bytes <= 4096) return launch_wide_tile<T, A, C, 8, 2, kWG, kNtS>(sg, k, st);
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
     // past the halo-only tile: the halo-only channel-per-lane look-ahead (round 5, in-process,

@@ -409,8 +409,12 @@ template <> struct ChanElem<int16_t> {
   }
 };
 
-template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false>
+// IP (XG only, the launcher's choice when the staged halo is exactly k frames): each output is
+// written in pass 2 over the x[n-k] it last read -- the same lane and address, as in the wide
+// look-ahead -- so no barrier before the output stage and no Q output registers
+template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false, bool IP = false>
 __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
+  static_assert(!IP || XG, "in-place outputs need the halo-only stage");
   using CE = ChanElem<T>;
   constexpr int E = CE::E;      // samples (channels) per dword
   constexpr int CL = C / E;     // dword columns per frame
@@ -596,35 +600,68 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   }
 
   // ---- pass 2: the prefix rebuilt from the stage, outputs ----
-  uint32_t yv[Q];
-#pragma unroll
-  for (int i = 0; i < Q; ++i) {
-    const uint32_t x = xv(i), xk = dword_at((f0 + i - k) * CL + c);
-    T y[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      base[e] += to_acc<A>(CE::get(x, e)) - to_acc<A>(CE::get(xk, e));
-      y[e] = to_out<T, A, DV>(base[e], p.o);
-    }
-    yv[i] = CE::put(y);
-  }
-  if (!tile_full) {  // the ragged last tile: element stores
-    const long long f = t0 + (long long)jl;
-#pragma unroll
-    for (int i = 0; i < Q; ++i)
-      if (f + i < nframes)
-#pragma unroll
-        for (int e = 0; e < E; ++e) out[(f + i) * C + c * E + e] = CE::get(yv[i], e);
-    return;
-  }
-  // ---- outputs through LDS (the stage layout), 1 KiB of contiguous output per store ----
-  __syncthreads();  // every read of the stage is done
   uint32_t* sww = reinterpret_cast<uint32_t*>(sb);
-  const int fo = (XG ? 0 : Hf) + jl;  // XG: the outputs take the halo region (Hg >= TG granules)
+  // the outputs in registers, then the ragged tile's element stores or the LDS output stage
+  auto pass2_regs = [&]() -> bool {
+    uint32_t yv[Q];
 #pragma unroll
-  for (int i = 0; i < Q; ++i) {
-    const int d = (fo + i) * CL + c;
-    sww[chan_slot<CL, Q>(d >> 2) * 4 + (d & 3)] = yv[i];
+    for (int i = 0; i < Q; ++i) {
+      const uint32_t x = xv(i), xk = dword_at((f0 + i - k) * CL + c);
+      T y[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        base[e] += to_acc<A>(CE::get(x, e)) - to_acc<A>(CE::get(xk, e));
+        y[e] = to_out<T, A, DV>(base[e], p.o);
+      }
+      yv[i] = CE::put(y);
+    }
+    if (!tile_full) {  // the ragged last tile: element stores
+      const long long f = t0 + (long long)jl;
+#pragma unroll
+      for (int i = 0; i < Q; ++i)
+        if (f + i < nframes)
+#pragma unroll
+          for (int e = 0; e < E; ++e) out[(f + i) * C + c * E + e] = CE::get(yv[i], e);
+      return false;
+    }
+    // ---- outputs through LDS (the stage layout), 1 KiB of contiguous output per store ----
+    __syncthreads();  // every read of the stage is done
+    const int fo = (XG ? 0 : Hf) + jl;  // XG: the outputs take the halo region (Hg >= TG granules)
+#pragma unroll
+    for (int i = 0; i < Q; ++i) {
+      const int d = (fo + i) * CL + c;
+      sww[chan_slot<CL, Q>(d >> 2) * 4 + (d & 3)] = yv[i];
+    }
+    return true;
+  };
+  if constexpr (IP) {
+    MAVG_DCHECK(Hf == k, "in-place chan tile: halo of exactly k frames", Hf, k);
+    if (!tile_full) {
+      pass2_regs();
+      return;
+    }
+    // the slot addresses from a value the compiler cannot prove equal to pass 1's (it would keep
+    // pass 1's Q addresses live across the carry), as in the wide look-ahead
+    int jx = jl;
+    asm volatile("" : "+v"(jx));
+#pragma unroll
+    for (int i = 0; i < Q; ++i) {
+      // groups of 8 frames the scheduler may not mix (the wide look-ahead's pass 2): bounded live
+      // LDS reads and fp64 conversions
+      if (i % 8 == 0 && i > 0) __builtin_amdgcn_sched_barrier(0);
+      const int d = (jx + i) * CL + c;  // = (f0 + i - k) CL + c: this lane's x[n-k], its output slot
+      uint32_t* sl = sww + chan_slot<CL, Q>(d >> 2) * 4 + (d & 3);
+      const uint32_t x = xv(i), xk = *sl;
+      T y[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        base[e] += to_acc<A>(CE::get(x, e)) - to_acc<A>(CE::get(xk, e));
+        y[e] = to_out<T, A, DV>(base[e], p.o);
+      }
+      *sl = CE::put(y);
+    }
+  } else {
+    if (!pass2_regs()) return;
   }
   // the wave reads back only its own frames: wave-level ordering suffices
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

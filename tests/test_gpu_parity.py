@@ -695,7 +695,9 @@ def test_chan_tile_halo_only_stage(oracle_mod, gpu, C, k):
     import torch
     frames = 9 * 1024 + 333
     plan = dsp.plan(frames * C, k, C, dsp.F32)
-    assert plan.startswith("chan_tile<") and ",xg=1>" in plan, plan
+    assert plan.startswith("chan_tile<") and ",xg=1" in plan, plan
+    # fp32 C = 4 with a halo of exactly k frames (whole 256-B rows) writes its outputs in place
+    assert (",ip=1>" in plan) == (C == 4 and (k * C) % 64 == 0), plan
     x = oracle_mod.synth_f32(frames * C, seed=k + C, dist=2)
     r = oracle_mod.check_synth_exact(_run(x, k, C, "blelloch", gpu), k, C, seed=k + C, dist=2, rtol=RTOL)
     assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, (plan, r)

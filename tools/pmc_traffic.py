@@ -62,7 +62,8 @@ def plan_key(plan):
     elif fam == "wide_tile":
         args = (T, acc, kv["C"], kv["P"], kv["U"], wg, kv["nt"], kv.get("dv", "0"))
     elif fam == "chan_tile":
-        args = (T, acc, kv["C"], kv["Q"], wg, kv["nt"], kv.get("dv", "0"), "true" if kv.get("xg", "0") == "1" else "false")
+        args = (T, acc, kv["C"], kv["Q"], wg, kv["nt"], kv.get("dv", "0"), "true" if kv.get("xg", "0") == "1" else "false",
+                "true" if kv.get("ip", "0") == "1" else "false")
     elif fam == "wide_ahead":
         args = (T, acc, kv["C"], kv["P"], kv["U"], wg, kv["nt"], kv.get("dv", "0"), kv["F"], kv["FU"],
                 "true" if kv.get("ch", "0") == "1" else "false", "true" if kv.get("xg", "0") == "1" else "false",

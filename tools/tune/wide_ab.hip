@@ -43,11 +43,12 @@ void add1(std::vector<Var>& vs, const Sig& sg, int k) {
   vs.push_back({name, [=](hipStream_t s) { return launch_wide_tile<T, A, C, P, U, WG, kNtS, DV>(sg, k, s); }, {}});
 }
 
-template <typename T, typename A, int C, int Q, int WG, bool XG = false, int NT = kNtSplit | kNtHalo | kNtStore>
+template <typename T, typename A, int C, int Q, int WG, bool XG = false, int NT = kNtSplit | kNtHalo | kNtStore,
+          bool IPOK = false>
 void addC(std::vector<Var>& vs, const Sig& sg, int k) {
   char name[64];
-  snprintf(name, sizeof name, "chan Q%d %d nt%d xg%d", Q, WG, NT, (int)XG);
-  vs.push_back({name, [=](hipStream_t s) { return launch_chan_tile<T, A, C, Q, WG, NT, 0, XG>(sg, k, s); }, {}});
+  snprintf(name, sizeof name, "chan Q%d %d nt%d xg%d%s", Q, WG, NT, (int)XG, XG && IPOK ? " ip" : "");
+  vs.push_back({name, [=](hipStream_t s) { return launch_chan_tile<T, A, C, Q, WG, NT, 0, XG, IPOK>(sg, k, s); }, {}});
 }
 
 // the round-3 unit kernels for the same C (tile_scan / ahead_scan, 32-B or 64-B units)
@@ -188,10 +189,12 @@ void add_wide_c(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     add1<T, A, C, 8, 1>(vs, sg, k);
     addC<T, A, C, 16, 256, true>(vs, sg, k);
     addC<T, A, C, 32, 256, true>(vs, sg, k);
+    addC<T, A, C, 32, 256, true, kNtSplit | kNtHalo | kNtStore, true>(vs, sg, k);
     addC<T, A, C, 16, 128, true>(vs, sg, k);
   } else {
     addC<T, A, C, 32, 256>(vs, sg, k);
     addC<T, A, C, 32, 256, true>(vs, sg, k);
+    addC<T, A, C, 32, 256, true, kNtSplit | kNtHalo | kNtStore, true>(vs, sg, k);
     addC<T, A, C, 32, 128, true>(vs, sg, k);
     addC<T, A, C, 16, 128, true>(vs, sg, k);
   }
@@ -254,6 +257,7 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     addC<T, A, C, 16, 128>(vs, sg, k);
     addC<T, A, C, 16, 256, true>(vs, sg, k);
     addC<T, A, C, 32, 256, true>(vs, sg, k);
+    addC<T, A, C, 32, 256, true, kNtSplit | kNtHalo | kNtStore, true>(vs, sg, k);
     addC<T, A, C, 16, 128, true>(vs, sg, k);
   }
 }
