@@ -241,11 +241,13 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     add1<T, A, C, 16, 1, 256, 1>(vs, sg, k);
   } else if constexpr (C == 4) {
     add1<T, A, C, 8, 1, 256, 0>(vs, sg, k);
+    add1<T, A, C, 8, 1, 256, 1>(vs, sg, k);  // the magic-multiply division
     add1<T, A, C, 16, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 8, 2, 256, 0>(vs, sg, k);
     add1<T, A, C, 8, 1, 512, 0>(vs, sg, k);  // 4096-frame tiles: a quarter of the tile's halo
   } else if constexpr (C == 8) {
     add1<T, A, C, 8, 1, 256, 0>(vs, sg, k);
+    add1<T, A, C, 8, 1, 256, 1>(vs, sg, k);  // the magic-multiply division
     add1<T, A, C, 4, 2, 256, 0>(vs, sg, k);
     // the halo-only channel-per-lane look-ahead (82 VGPRs) at tile-scan windows too
     addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 384);
