@@ -6,6 +6,9 @@
 //
 // build: make -C tools/tune wide_ab
 // run:   tools/tune/wide_ab <log2n> <k> <C> [rounds] [dist] [f32|i16] [hs]
+// A copy of this file built against another tree's headers (round 5's wide_ab_prev / _cand /
+// _r04) compares that tree's kernels with this library's: the library is linked -Bsymbolic, so
+// its launches keep its own kernel code even where the template instances share a name.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
