@@ -19,13 +19,16 @@ Rank 0 prints ONE JSON line (contract in the task statement), with
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import signal
 import socket
 import statistics
+import shutil
 import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -73,6 +76,10 @@ WORKLOADS = {
     "f32_c4_long": (1 << 30, 44100, 4, "f32", "blelloch"),
     "f32_c8_long": (1 << 30, 44100, 8, "f32", "blelloch"),
     "f32_c8_k2048": (1 << 30, 2048, 8, "f32", "blelloch"),
+    # the in-place halo-only channel tile (fp32 C = 4) and the int16 dword-column channel tile
+    # (C = 8) at the window where each is dispatched
+    "f32_c4_k2048": (1 << 30, 2048, 4, "f32", "blelloch"),
+    "i16_c8_k2048": (1 << 30, 2048, 8, "i16", "blelloch"),
     "i16_c4_2p30": (1 << 30, 1024, 4, "i16", "blelloch"),
     "i16_c8_2p30": (1 << 30, 1024, 8, "i16", "blelloch"),
     "i16_c4_long": (1 << 30, 44100, 4, "i16", "blelloch"),
@@ -80,7 +87,7 @@ WORKLOADS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -102,7 +109,16 @@ def parse():
                          "against the CPU oracle")
     ap.add_argument("--all-workloads", action="store_true",
                     help="print one extra JSON line per secondary workload (rank 0, N=1 only)")
-    return ap.parse_args()
+    # N > 1 failure bounds (DESIGN.md "Multi-GPU"): a peer that never arrives ends the run with
+    # status 124 and a line naming the rank and the phase, instead of a hang past the driver's limit
+    ap.add_argument("--init-timeout", type=float, default=300.0,
+                    help="N>1: seconds a rank may wait in the rendezvous (init_process_group)")
+    ap.add_argument("--phase-timeout", type=float, default=120.0,
+                    help="N>1: seconds a rank may spend in any later phase (halo exchange, barrier, all-gather)")
+    ap.add_argument("--launch-deadline", type=float, default=None,
+                    help="--gpus N without a launcher: seconds before the parent kills its ranks "
+                         "(default: derived from --steps/--warmup, the workloads and the timeouts)")
+    return ap.parse_args(argv)
 
 
 def _free_port() -> int:
@@ -121,42 +137,102 @@ def rank_env(base: dict, rank: int, world: int, port: int) -> dict:
     return env
 
 
-def self_launch(argv, world: int, timeout: float = None) -> int:
+def run_deadline(args) -> float:
+    """Seconds `bench.py --gpus N` (self-launched ranks) may run before the
+    parent kills its ranks: the rendezvous and one stuck phase (each rank's
+    own watchdog fires first), plus, per workload, its warm-up and timed steps
+    twice over (the sharded steps, then shard_timing's single launches) at a
+    generous 50 ms each, the copy calibration, the check and the all-gathers,
+    plus the CPU baseline's repetitions where one runs (N = 1 only)."""
+    n_work = len(WORKLOADS) if args.all_workloads else 1
+    per_workload = 60.0 + (2 * args.steps + 2 * args.warmup) * 0.05
+    cpu = 0.0 if (args.no_cpu_baseline or args.gpus > 1) else 30.0 * (args.cpu_reps + max(3, args.cpu_reps))
+    return args.init_timeout + args.phase_timeout + n_work * per_workload + cpu
+
+
+def self_launch(argv, world: int, timeout: float = None, script: str = None) -> int:
     """`bench.py --gpus N` without a launcher: start N fresh child ranks (this
     process has not touched the GPU and never does), wait for all of them and
-    return the worst exit status.  If one rank fails the others are stopped
-    (they would wait forever in the next collective).  Rank 0's stdout is the
-    one JSON line."""
+    return the exit status of the first rank that failed (0 if none did).  If
+    one rank fails the others are stopped (they would wait forever in the next
+    collective).  Past `timeout` seconds
+    every rank still running is killed, stderr names each rank's last phase
+    (the ranks' PhaseWatchdog records, deadline.py) and the status is 124.
+    Rank 0's stdout is the one JSON line.  `script`: the program each rank
+    runs (default this file; tests pass a fault-injection worker)."""
+    from digital_signal_processsing_amd.deadline import EXIT_TIMEOUT, describe_phases, read_phases
     port = _free_port()
-    me = os.path.abspath(__file__)
-    procs = [subprocess.Popen([sys.executable, "-u", me] + list(argv), env=rank_env(os.environ, r, world, port))
-             for r in range(world)]
+    me = os.path.abspath(script or __file__)
+    sdir = tempfile.mkdtemp(prefix="mavg_bench_")
+    procs = []
+    for r in range(world):
+        env = rank_env(os.environ, r, world, port)
+        env["MAVG_BENCH_STATUS_DIR"] = sdir
+        procs.append(subprocess.Popen([sys.executable, "-u", me] + list(argv), env=env))
     deadline = None if timeout is None else time.monotonic() + timeout
-    worst = 0
+    first = 0  # the status of the first rank that failed: the cause, not the SIGTERMs that follow it
     live = list(procs)
-    while live:
-        for p in list(live):
-            rc = p.poll()
-            if rc is None:
-                continue
-            live.remove(p)
-            rc = 128 - rc if rc < 0 else rc
-            worst = max(worst, rc)
-            if rc != 0:
-                for q in live:  # the exact child PIDs this function started
-                    q.send_signal(signal.SIGTERM)
-        if deadline is not None and time.monotonic() > deadline:
-            for q in live:
+    try:
+        while live:
+            for p in list(live):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                live.remove(p)
+                rc = 128 - rc if rc < 0 else rc
+                if rc != 0 and first == 0:
+                    first = rc
+                    for q in live:  # the exact child PIDs this function started
+                        q.send_signal(signal.SIGTERM)
+            if deadline is not None and live and time.monotonic() > deadline:
+                ranks = [procs.index(q) for q in live]
+                print(f"mavg-bench: launch deadline of {timeout:.0f} s expired with ranks {ranks} still running; "
+                      f"{describe_phases(read_phases(sdir))}; killing them", file=sys.stderr, flush=True)
+                for q in live:
+                    q.kill()
+                first = first or EXIT_TIMEOUT
+                deadline = None
+            time.sleep(0.05)
+    finally:
+        for q in live:
+            if q.poll() is None:
                 q.kill()
-            worst = max(worst, 124)
-            deadline = None
-        time.sleep(0.05)
-    return worst
+        shutil.rmtree(sdir, ignore_errors=True)
+    return first
 
 
-def init_dist(args):
+class _NoWatchdog:
+    """N = 1: no peer to wait for, no watchdog thread beside the timed loop."""
+
+    def set(self, *a, **kw):
+        pass
+
+    def phase(self, *a, **kw):
+        return _nullcontext()
+
+    def stop(self):
+        pass
+
+
+class _nullcontext:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+def make_watchdog(world: int):
+    if world <= 1:
+        return _NoWatchdog()
+    from digital_signal_processsing_amd.deadline import PhaseWatchdog
+    return PhaseWatchdog(int(os.environ.get("RANK", "0")), world)
+
+
+def init_dist(args, wd=None):
     import torch
     import torch.distributed as dist
+    wd = wd or _NoWatchdog()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -167,10 +243,16 @@ def init_dist(args):
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
+        # the communicator's own timeout (RCCL's watchdog, gloo's waits) backs up the
+        # rank's PhaseWatchdog, whose budgets are shorter so that its line comes first
+        tmo = datetime.timedelta(seconds=max(args.init_timeout, args.phase_timeout) + 60.0)
+        with wd.phase("init (rendezvous)", args.init_timeout):
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
+            else:
+                dist.init_process_group("gloo", timeout=tmo)
+            # the first collective: a communicator that cannot connect fails here, bounded
+            dist.barrier()
     return rank, world, local
 
 
@@ -413,6 +495,7 @@ def copy_ceiling(xs, ys, rot, steps, world, min_s=0.25):
     import digital_signal_processsing_amd as dsp
     for w in range(3):
         dsp.stream_copy(xs[w % rot], ys[w % rot])
+    torch.cuda.synchronize()
     times, t0 = [], time.perf_counter()
     while len(times) < steps or time.perf_counter() - t0 < min_s:
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
@@ -422,10 +505,22 @@ def copy_ceiling(xs, ys, rot, steps, world, min_s=0.25):
             b.record()
         torch.cuda.synchronize()
         times += [a.elapsed_time(b) for a, b in ev]
-    return max_over_ranks(statistics.mean(times), world), len(times)
+    return max_over_ranks(statistics.mean(times), world), len(times), time.perf_counter() - t0
 
 
-def run_workload(args, name, rank, world, with_cpu):
+def halo_progress(hev):
+    """Watchdog detail for a wait after the timed steps (RCCL: the halo receive
+    is a stream wait, so a missing send shows up in the synchronize): the first
+    timed step whose head launch the launch stream has not reached."""
+    if not hev:
+        return ""
+    for i, (h0, _) in enumerate(hev):
+        if not h0.query():
+            return f" -- the launch stream has not passed the halo wait of timed step {i} (its head launch not started)"
+    return " -- every timed step's halo wait has been passed on the launch stream"
+
+
+def run_workload(args, name, rank, world, with_cpu, wd=None):
     import torch
     import digital_signal_processsing_amd as dsp
     from digital_signal_processsing_amd.shard import sharded_moving_average
@@ -462,7 +557,10 @@ def run_workload(args, name, rank, world, with_cpu):
     # otherwise still timed on the clock ramp (i16_c4_2p30 0.670 of peak after
     # 5 warm-up steps, 0.777 after 200; the headline 0.786 / 0.807;
     # profiles/r05_validation/warmup_ramp/).  The timed region is unchanged.
-    copy_ms, copy_launches = copy_ceiling(xs, ys, rot, args.steps, world)
+    wd = wd or _NoWatchdog()
+    pt = args.phase_timeout
+    with wd.phase(f"{name}: copy calibration (all-reduce)", pt):
+        copy_ms, copy_launches, copy_s = copy_ceiling(xs, ys, rot, args.steps, world)
 
     def step(i=None, j=0):
         if world > 1:
@@ -478,14 +576,19 @@ def run_workload(args, name, rank, world, with_cpu):
         if i is not None:
             ev[i][1].record()
 
-    for w in range(args.warmup):
-        step(j=w % rot)
-    barrier(world)
+    with wd.phase(f"{name}: warm-up steps (halo exchange)", pt):
+        for w in range(args.warmup):
+            step(j=w % rot)
+    with wd.phase(f"{name}: barrier before the timed steps", pt):
+        barrier(world)
+    wd.set(f"{name}: timed steps (halo exchange)", pt)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    wd.set(f"{name}: barrier after the timed steps (halo wait on the stream)", pt, lambda: halo_progress(hev))
     barrier(world)
     dt_s = time.perf_counter() - t0
+    wd.set(f"{name}: all-reduce of the timings", pt)
     dt_s = max_over_ranks(dt_s, world)
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     kern_avg_ms = statistics.mean(kern_ms)
@@ -544,7 +647,9 @@ def run_workload(args, name, rank, world, with_cpu):
         },
     }
     if args.check:
+        wd.set(f"{name}: check against the oracle", pt)
         res = check_output(y, n, k, C, dt, seed, rank)
+        wd.set(f"{name}: all-gather of the checks", pt)
         if world > 1:
             import torch.distributed as dist
             allres = [None] * world
@@ -553,9 +658,12 @@ def run_workload(args, name, rank, world, with_cpu):
                    "mismatches": sum(r["mismatches"] for r in allres)}
         line["check"] = res
     if world > 1:
+        wd.set(f"{name}: all-gather of the device records", pt)
         line["rccl"] = comm_report(rank, world, (k - 1) * C * elem)
     if world > 1:  # after --check: the single launches overwrite the output with a no-halo result
+        wd.set(f"{name}: single-launch timing (barrier, all-gather)", pt)
         line["scaling_detail"] = shard_timing(args, x, y, k, C, algo, ev, hev, value, n, rank, world)
+    wd.set(f"{name}: report", None)
     copy_gbs = 2 * elem * n / (copy_ms * 1e-3) / 1e9
     line["copy_ceiling"] = {
         "kernel": "mavg_stream_copy: flat grid, one 16-B non-temporal load + store per thread",
@@ -564,8 +672,14 @@ def run_workload(args, name, rank, world, with_cpu):
         "frac": round(copy_gbs / HBM_PEAK_GBS, 4),
         "kernel_avg_ms": round(copy_ms, 4),
         "launches": copy_launches,
+        "seconds": round(copy_s, 3),
         "when": "measured before the workload's warm-up steps, over at least --steps launches and 0.25 s",
     }
+    # what ran on the device before the timed steps (bench lines from round 5 on: the copy
+    # calibration first, which also takes the device out of its idle clocks; earlier rounds'
+    # lines had only the W warm-up steps -- DESIGN.md "The start of a process")
+    line["warmup_detail"] = {"copy_calibration_launches": copy_launches, "copy_calibration_s": round(copy_s, 3),
+                             "workload_warmup_steps": args.warmup}
     line["roofline"]["frac_of_copy"] = round(achieved / copy_gbs, 4)
     if with_cpu and rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"], line["cpu_baseline_multicore"] = cpu_baseline(args, n, k, C, seed)
@@ -577,9 +691,11 @@ def run_workload(args, name, rank, world, with_cpu):
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(self_launch(sys.argv[1:], args.gpus))
-    rank, world, _ = init_dist(args)
-    line = run_workload(args, args.workload, rank, world, with_cpu=True)
+        deadline = args.launch_deadline if args.launch_deadline is not None else run_deadline(args)
+        sys.exit(self_launch(sys.argv[1:], args.gpus, timeout=deadline))
+    wd = make_watchdog(int(os.environ.get("WORLD_SIZE", "1")))
+    rank, world, _ = init_dist(args, wd)
+    line = run_workload(args, args.workload, rank, world, with_cpu=True, wd=wd)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if args.all_workloads and world == 1:
@@ -589,7 +705,9 @@ def main():
                 print(json.dumps(extra), file=sys.stderr, flush=True)
     if world > 1:
         import torch.distributed as dist
-        dist.destroy_process_group()
+        with wd.phase("destroy_process_group", args.phase_timeout):
+            dist.destroy_process_group()
+    wd.stop()
 
 
 if __name__ == "__main__":

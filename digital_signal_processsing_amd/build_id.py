@@ -5,8 +5,12 @@ from (csrc/*.hip, csrc/*.hpp, csrc/Makefile, include/*.h), in name order.
 csrc/Makefile runs this script and links the id into the library
 (`mavg_build_id()`, include/mavg.h); `__graft_entry__.build()`, `smoke()` and
 tests/test_abi.py compare the loaded library's id with the tree's, so a
-prebuilt library that was not compiled from these sources is caught.  Plain
-Python, no imports beyond the standard library (the Makefile runs it)."""
+prebuilt library linked from other sources is caught.  The Makefile also makes
+every object depend on a stamp named after this id and a hash of the compile
+flags, so objects are recompiled whenever either changes (stale objects with
+newer mtimes are not relinked under a fresh id).  The id names the sources
+only: the release, debug and hooks libraries share it and differ in flags.
+Plain Python, no imports beyond the standard library (the Makefile runs it)."""
 from __future__ import annotations
 
 import glob

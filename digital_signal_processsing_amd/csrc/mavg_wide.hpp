@@ -708,9 +708,11 @@ namespace mavg {
 // read: half the LDS per workgroup (C = 8, 1024-frame tiles: 33 KiB instead of
 // 65 KiB, four workgroups per CU instead of two).
 // MW: the minimum waves per SIMD the register allocation must allow (0: no
-// bound).  The halo-only form is LDS-sized for 4 (C = 8, 256 threads: 33 KiB,
-// four workgroups per CU), which the unbounded schedule misses by converting
-// every loaded value to fp64 at once.
+// bound).  A tuning parameter only: every dispatch in the library passes 0
+// (tools/tune/wide_ab.hip's `mw` variants A/B it).  The bound was measured when
+// the halo-only form held 142-228 VGPRs (forcing 128 for fp32 C = 4 spilled,
+// 0.612 -> 0.50 of peak); the register work that followed (126 VGPRs at C = 8,
+// 92 at C = 4) reaches the LDS-sized 4 workgroups per CU without it.
 template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false,
           bool XG = false, int MW = 0>
 __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadParams p) {

@@ -38,11 +38,16 @@ CONFIGS = [
     ("f32_c4_2p30_k44100", 1 << 30, 44100, 4, "f32", "blelloch"),
     ("f32_c8_2p30_k44100", 1 << 30, 44100, 8, "f32", "blelloch"),
     ("f32_c8_2p30_k2048", 1 << 30, 2048, 8, "f32", "blelloch"),
+    # the in-place halo-only chan tile (fp32 C = 4, 2048 <= k <= 3584, k % 16 == 0: each output
+    # written over the x[n-k] it last read) at full size: large grids and the XCD remap
+    ("f32_c4_2p30_k2048", 1 << 30, 2048, 4, "f32", "blelloch"),
     # the reference's int16 PCM at 4 and 8 channels (wav_header.h:26-48)
     ("i16_c4_2p30_k1024", 1 << 30, 1024, 4, "i16", "blelloch"),
     ("i16_c8_2p30_k1024", 1 << 30, 1024, 8, "i16", "blelloch"),
     ("i16_c4_2p30_k44100", 1 << 30, 44100, 4, "i16", "blelloch"),
     ("i16_c8_2p30_k44100", 1 << 30, 44100, 8, "i16", "blelloch"),
+    # the int16 dword-column chan tile (C = 8, 2048 <= k <= 3072) at full size
+    ("i16_c8_2p30_k2048", 1 << 30, 2048, 8, "i16", "blelloch"),
 ]
 
 

@@ -73,14 +73,18 @@ void addA(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D = 1024
 }
 
 // the look-ahead scan with U units per lane (tile = U * WG * F frames), as dispatched otherwise
+// self: self-published records (AheadParams::self) -- no phase A; every tile publishes its own
+// record (its aggregate) as soon as its loads land and the carry reads the records after the
+// in-tile scan (round 6: the aggregate-first form for the int16 long windows)
 template <typename T, typename A, int C, int F, int U, bool RC, bool WREC, bool RUNS>
-void addU(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D, size_t lds_floor = 0) {
+void addU(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D, size_t lds_floor = 0, bool self = false) {
   constexpr int kNtA = kNtStore | kNtHalo;
   char name[80];
-  snprintf(name, sizeof name, "ahead U%d wrec=%d runs=%d D%d lds>=%zu", U, (int)WREC, (int)RUNS, D, lds_floor);
+  snprintf(name, sizeof name, "ahead U%d wrec=%d runs=%d D%d lds>=%zu%s", U, (int)WREC, (int)RUNS, D, lds_floor,
+           self ? " self" : "");
   vs.push_back({name, [=](hipStream_t s) {
                   return launch_ahead_scan<T, A, C, F, U, kNtA, RC, true, WREC, 0, false, RUNS, 256>(sg, k, s, ws, D,
-                                                                                                   false, lds_floor);
+                                                                                                   self, lds_floor);
                 }, {}});
 }
 
@@ -213,11 +217,20 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   if (k > 8192) {  // the look-ahead range
     if constexpr (C == 1) {  // mono: per-wave records, D = 512 (the library's dispatch)
       addU<T, A, C, 8, 4, false, true, false>(vs, sg, k, ws, 512);
+      // aggregate-first (self-published records) against the look-ahead
+      addU<T, A, C, 8, 4, false, true, false>(vs, sg, k, ws, 512, 0, true);
+      addU<T, A, C, 8, 4, false, false, false>(vs, sg, k, ws, 512, 0, true);
+      addU<T, A, C, 8, 8, false, false, false>(vs, sg, k, ws, 256, 0, true);
+      addU<T, A, C, 8, 2, false, true, false>(vs, sg, k, ws, 512, 0, true);
       addU<T, A, C, 8, 4, false, true, false>(vs, sg, k, ws, 384);
       addU<T, A, C, 8, 8, false, false, false>(vs, sg, k, ws, 256);
       addU<T, A, C, 8, 8, false, false, false>(vs, sg, k, ws, 192);
     } else if constexpr (C == 2) {
       addU<T, A, C, 4, 8, false, false, false>(vs, sg, k, ws, 256);
+      // aggregate-first (self-published records) against the look-ahead
+      addU<T, A, C, 4, 8, false, false, false>(vs, sg, k, ws, 256, 0, true);
+      addU<T, A, C, 4, 4, false, false, false>(vs, sg, k, ws, 512, 0, true);
+      addU<T, A, C, 4, 4, false, true, false>(vs, sg, k, ws, 512, 0, true);
       addU<T, A, C, 4, 4, true, false, false>(vs, sg, k, ws, 768);   // recompute-from-registers (RC)
       addU<T, A, C, 4, 8, true, false, false>(vs, sg, k, ws, 256);
       addU<T, A, C, 4, 4, false, true, false>(vs, sg, k, ws, 512);   // per-wave records for stereo
