@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 // Debug build (make -C csrc debug -> libmavg_debug.so): device bounds checks on LDS
 // stage indices, x[n-k] extractions, tile indices and record slots; a failed
 // check prints (what, block, thread, two values) and traps.  Compiled out of

@@ -301,6 +301,22 @@ constexpr long long kAheadU8MaxTiles = 1024;
 inline bool ahead_past_l2(long long k, int C, int elem, int TF) {
   return k * C * elem > (1LL << 21) && k >= 8LL * TF;
 }
+// The windows that take the aggregate-first look-ahead (dispatch_ahead; 16-B units, 32-KiB
+// tiles of U = 8 x 256 threads): int16 mono / stereo past a 16-KiB halo, int16 4 channels past
+// 64 KiB, fp32 stereo past 32 KiB (the wide tile's), each short of the L2 reach (window-matched
+// runs take over there) and int16 mono up to k = 131072 (5e5 measured 0.641 -> 0.624).
+template <typename T, int C>
+inline bool agg_first_range(long long k) {
+  constexpr int F = 16 / (C * (int)sizeof(T));
+  constexpr int TF8 = kWG * F * 8;
+  const long long halo = k * C * (long long)sizeof(T);
+  if (ahead_past_l2(k, C, sizeof(T), TF8)) return false;
+  if constexpr (sizeof(T) == 2 && C <= 2) return halo > 16384 && (C == 2 || k <= 131072);
+  if constexpr (sizeof(T) == 2 && C == 4) return halo > 65536;
+  if constexpr (sizeof(T) == 4 && C == 2) return halo > 32768;
+  return false;
+}
+
 template <typename T, typename A, int C, int F, int U, int NT, bool RC, bool DMA, bool WREC, int DV = 0, bool HS = false,
           bool RUNS = false, int WG = kWG>
 // lds_floor: the LDS the launch allocates at least (fewer workgroups per CU, a footprint cap; 0: none)
@@ -436,6 +452,31 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   //     1e5 0.527 -> 0.572.
   //   int16 mono (16384-frame tiles) lost in the tuner (0.680 -> 0.667).
   // (16-B units only: the frame-unit form of element-aligned views keeps U = 4)
+  // Aggregate-first records (round 6): int16 mono / stereo / 4 channels and fp32 stereo take
+  // 32-KiB tiles (U = 8 x 256 threads: 16384 / 8192 / 4096 frames) with self-published records --
+  // no phase A; each tile publishes its own aggregate as soon as its loads land, and the carry reads
+  // the records after its in-tile scan.  With tiles this long a window spans few of them, and the
+  // nearest ones are out before the scan is done; with 4096-frame mono tiles the same mode loses
+  // (round 3, and again here).  In-process A/B against the library's dispatch, 2^30 samples,
+  // fraction of 8 TB/s (tools/tune/wide_ab.hip "self", profiles/r06_tuning/self/):
+  //   int16 mono   k=10000 0.711 -> 0.730 (the 1024-thread tile), 12000 0.706 -> 0.733, 20000
+  //                0.647 -> 0.673, 44100 0.666 -> 0.698, 1e5 0.638 -> 0.648, 2e5 0.638 -> 0.640
+  //                (k <= 131072 here), 5e5 0.641 -> 0.624; the tile keeps k <= 8192 (0.756 vs 0.734)
+  //   int16 stereo k=8192 0.657 -> 0.711, 12000 0.614 -> 0.714, 44100 0.640 -> 0.702, 2e5 0.574 ->
+  //                0.702; the tile keeps k <= 4096 (0.747 vs 0.716)
+  //   int16 C = 4  k=20000 0.607 -> 0.628, 44100 0.597 -> 0.626, 1e5 0.484 -> 0.619 (against the
+  //                wide look-ahead, and the 4096-frame look-ahead past int32 sums); k=8192 a tie
+  //   fp32 stereo  k=20000 0.661 -> 0.691, 44100 0.651 -> 0.689, 1e5 0.647 -> 0.691 (against the
+  //                wide look-ahead)
+  // Not taken: fp32 mono (k=20000 0.730 vs 0.696, 44100 0.718 vs 0.688), fp32 / int16 with 4 / 8
+  // channels in 1-frame units (0.42 / 0.48 against the channel-per-lane look-ahead's 0.62 / 0.59),
+  // the Hillis-Steele flavour (k=44100 0.593 vs 0.574).
+  constexpr bool kAgg = !HS && U0 == 4 && F * C * (int)sizeof(T) == 16 &&
+                        ((sizeof(T) == 2 && C <= 4) || (sizeof(T) == 4 && C == 2));
+  if constexpr (kAgg) {
+    if (agg_first_range<T, C>(k))
+      return launch_ahead_scan<T, A, C, F, 8, kNtA, false, true, false, 0, false, false, WG>(sg, k, st, ws, 256, true);
+  }
   constexpr bool kU8 = !HS && U0 == 4 && F * C * (int)sizeof(T) == 16 &&
                        ((sizeof(T) == 4 && C == 1) || (sizeof(T) == 2 && C == 2));
   if constexpr (kU8) {
@@ -473,9 +514,11 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
 // wide look-ahead scan (mavg_wide.hpp): the look-ahead record carry in its
 // unit layout (F frames x U units per lane, per-tile records) with the wide
 // in-tile scan (P-frame chunks x UW rows); 16-B-aligned views only.
+// self: aggregate-first (self-published) records, the int16 halo-only CH form only (wide_ahead_kernel)
 template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false,
           bool XG = false, int MW = 0>
-int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
+int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead, bool self = false) {
+  if (self && !(CH && XG && std::is_integral<T>::value)) return MAVG_ERR_UNSUPPORTED;
   constexpr int NW = WG / 64;
   constexpr int EPG = 16 / (int)sizeof(T);
   constexpr int CL = C * (int)sizeof(T) / 4 > 0 ? C * (int)sizeof(T) / 4 : 1;  // CH: dword columns per frame
@@ -514,9 +557,9 @@ int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
              "wide_ahead<%s,acc=%s,C=%d,P=%d,U=%d,nt=%d,dv=%d,F=%d,FU=%d%s%s,mw=%d> grid=%lld block=%d lds=%zu "
-             "tile_frames=%d ahead=%d remap=%d ws=%zu",
+             "tile_frames=%d ahead=%d remap=%d%s ws=%zu",
              type_name<T>(), type_name<A>(), C, P, UW, NT, DV, F, U, CH ? ",ch=1" : "", XG ? ",xg=1" : "", MW, ntiles,
-             WG, lds, TF, ahead, xcd_remap, need);
+             WG, lds, TF, ahead, xcd_remap, self ? " self=1" : "", need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
   }
@@ -540,7 +583,7 @@ int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.ahead = ahead;
   p.head = xcd_remap == 1 ? (int)std::min<long long>((long long)k / TF, nfull) : 0;
   p.spin = spin;
-  p.self = 0;
+  p.self = self ? 1 : 0;
   p.gran = static_cast<unsigned long long*>(ws.ptr);
   p.runs = nullptr;
   p.stats = static_cast<unsigned char*>(ws.ptr) + need - trace_bytes - 16;
@@ -618,6 +661,11 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
     // Longer halos take bigger workgroups: the LDS stage per workgroup then
     // carries more waves (tools/tune/sweep_wg.sh, sweep_wg2.sh).
     if constexpr (sizeof(T) == 2) {
+      // past a 16-KiB halo int16 mono / stereo take the aggregate-first look-ahead
+      // (dispatch_ahead, round 6) instead of the 1024-thread tile
+      if constexpr (kUnitBytes == 16 && C <= 2) {
+        if (block == 0 && agg_first_range<T, C>(k)) return dispatch_ahead<T, A, C, F>(sg, k, st, ws);
+      }
       // int16 keeps register staging: LDS-DMA tiles won the in-process tuner's
       // A/B (mono U2 x 512 0.811-0.820 vs 0.800-0.803) but lost 2-3.5 % in
       // bench.py's own timing, one HIP-event pair per back-to-back launch
@@ -712,6 +760,8 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   if constexpr (sizeof(T) == 4 && C == 2) {
     if (halo_bytes <= 2048) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 16, 1, kWG, kNtS>(sg, k, st);
+    // the unit kernels' aggregate-first look-ahead (dispatch_ahead, round 6) short of the L2 reach
+    if (agg_first_range<T, C>(k)) return MAVG_ERR_UNSUPPORTED;
     return launch_wide_ahead<T, A, C, 8, 1, kWG, kNtA, 0, 2, 4>(sg, k, st, ws, 512);
   } else if constexpr (sizeof(T) == 4 && C == 4) {
     // 2048 <= k <= 3584: the halo-only channel-per-lane tile (2048-frame tiles; in-process,
@@ -754,6 +804,8 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     if constexpr (sizeof(A) == 4) {
       if (halo_bytes <= 8192) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
       if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 16, 1, kWG, kNtS>(sg, k, st);
+      // past 64 KiB the unit kernels' aggregate-first look-ahead (dispatch_ahead, round 6)
+      if (agg_first_range<T, C>(k)) return MAVG_ERR_UNSUPPORTED;
       // past it the wide look-ahead (64-B chunks, D = 512) instead of the 16-B unit look-ahead
       // (in-process A/B, profiles/r04_tuning/wide/wide_i16_c4_*: k=44100 0.579 -> 0.598, 20000
       // 0.590 -> 0.602; bench timing, bit-exact, profiles/r04_tuning/wide/bench_timing_i16_c4_*:

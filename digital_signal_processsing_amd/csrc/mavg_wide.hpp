@@ -788,7 +788,14 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   const unsigned nb = gridDim.x;
   const unsigned bd = blockIdx.x + (unsigned)p.ahead;
   const long long ja = bd < nb ? map_tile(bd) : -1;
-  const bool produce = ja >= 0 && ja < p.nfull;
+  // SELF (round 6, int16 halo-only CH form only; AheadParams::self): aggregate-first records --
+  // no phase A; every tile publishes its own record from the x it holds in registers as soon as
+  // its loads land, and the carry reads the records after the in-tile scan.  Integer sums are
+  // exact, so a record summed in the lane / butterfly order here has the bits of the producer's
+  // and the recompute path's sequences: the output is the same under every schedule.
+  constexpr bool kSelfOk = CH && XG && std::is_integral<T>::value;
+  const bool self = kSelfOk && p.self != 0;
+  const bool produce = !self && ja >= 0 && ja < p.nfull;
   // XG: the lane's x (dword column cl -- channels cl*E .. cl*E + E - 1 -- of frames j0 .. j0 + P - 1)
   const int cl = lane & (CL - 1);  // CH: the lane's dword column
   const int j0 = w * WF + (lane / CL) * P;
@@ -870,11 +877,29 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
     share(0, r);
   }
   if (tid == 0) MAVG_ATRACE(1, MAVG_ANOW());
-  const bool own = blockIdx.x < (unsigned)p.ahead && tile < p.nfull;  // no block D slots earlier
+  const bool own = (self || blockIdx.x < (unsigned)p.ahead) && tile < p.nfull;  // no block D slots earlier
   if (own) {
-    SA r[C];
-    wave_record_lean<T, SA, C, F, U, WG>(in, tile, w, lane, false, r);
-    share(1, r);
+    if constexpr (kSelfOk) {
+      if (self) {  // the lane's column sums, then butterflies over the lanes of one column
+        SA sc[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          sc[e] = (SA)0;
+#pragma unroll
+          for (int i = 0; i < P; ++i) sc[e] += to_acc<SA>(CEl::get(xr[i], e));
+#pragma unroll
+          for (int sh = CL; sh < 64; sh <<= 1) sc[e] += __shfl_xor(sc[e], sh, 64);
+        }
+        if (lane < CL)
+#pragma unroll
+          for (int e = 0; e < E; ++e) shares[(1 * NW + w) * C + lane * E + e] = sc[e];
+      }
+    }
+    if (!self) {
+      SA r[C];
+      wave_record_lean<T, SA, C, F, U, WG>(in, tile, w, lane, false, r);
+      share(1, r);
+    }
   }
   long long jh = -1;
   if (p.xcd_remap == 1) {
@@ -900,7 +925,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
     for (int h = 0; h < NG; ++h) v[h] = gran_load(gran + (qlo * C + sl) * NG + h);
   };
   MAVG_DCHECK(qhi <= p.nfull, "wide record read range", qhi, p.nfull);
-  if (tid < nslot) {
+  if (!self && tid < nslot) {
     slot_load(tid, rv);
   } else {
 #pragma unroll
@@ -1082,7 +1107,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   for (long long sb0 = 0; sb0 < nslot; sb0 += WG) {
     const long long sl = sb0 + tid;
     const bool act = sl < nslot;
-    if (sb0 != 0) {
+    if (sb0 != 0 || self) {
       if (act) {
         slot_load(sl, rv);
       } else {

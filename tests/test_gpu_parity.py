@@ -585,6 +585,53 @@ def test_self_published_records(oracle_mod, gpu, k):
     assert_f32_close(_run(xf[cut:], k, 1, "blelloch", gpu, history=hist), full[cut:], f"k={k} history")
 
 
+@pytest.mark.parametrize("dtype,C,k", [("i16", 1, 8_193), ("i16", 1, 44_100), ("i16", 1, 131_072),
+                                       ("i16", 2, 4_097), ("i16", 2, 200_000), ("i16", 4, 8_193),
+                                       ("i16", 4, 100_000), ("f32", 2, 4_097), ("f32", 2, 100_000)])
+def test_aggregate_first_records(oracle_mod, gpu, dtype, C, k):
+    """int16 mono / stereo / 4 channels and fp32 stereo windows past their tiles' LDS
+    halo run the look-ahead scan in 32-KiB tiles with aggregate-first records (no
+    phase A: every tile publishes its own record as soon as its loads land, the
+    carry reads the records after the in-tile scan): the first window past each
+    range boundary and long ones, bitwise the same under a forced recompute, absent
+    and minimal look-ahead (head duty only), int16 bit-exact against the oracle,
+    fp32 rounding data (dist 2) within the bar against the exact sums, and a
+    history (the window reaching before frame 0)."""
+    import digital_signal_processsing_amd as dsp
+    dt = dsp.F32 if dtype == "f32" else dsp.I16
+    frames = 3_000_017 // C  # hundreds of tiles: ragged XCD runs, head duty
+    plan = dsp.plan(frames * C, k, C, dt)
+    assert plan.startswith("ahead_scan<") and "self=1" in plan and "U=8" in plan and "wrec=0" in plan, plan
+    tf = int(plan.split("tile_frames=")[1].split()[0])
+    assert tf * C * (4 if dtype == "f32" else 2) == 32768, plan
+    if k in (4_097, 8_193):  # the first window of the range: the one before it keeps its kernel
+        prev = dsp.plan(frames * C, k - 1, C, dt)
+        assert "self=1" not in prev, prev
+    if dtype == "f32":
+        x = oracle_mod.synth_f32(frames * C, seed=93, dist=2)
+    else:
+        x = oracle_mod.synth_i16(frames * C, seed=93)
+    base = _run(x, k, C, "auto", gpu)
+    for sched in ({"spin": 0}, {"slots": 0}, {"slots": 8, "spin": 0}):
+        y = _with_schedule(sched, lambda lib: _run(x, k, C, "auto", gpu, library=lib))
+        assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), sched
+    if dtype == "f32":
+        r = oracle_mod.check_synth_exact(base, k, C, seed=93, dist=2, rtol=RTOL)
+        assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, r
+    else:
+        assert np.array_equal(base, oracle_mod.mavg_i16(x, k, C))
+    cut = k + 4_321  # a history: the concatenation property through the aggregate-first carry
+    n2 = min(frames, cut + 300_000)
+    xs = x[: n2 * C]
+    full = _run(xs, k, C, "auto", gpu)
+    hist = xs[(cut - (k - 1)) * C: cut * C].copy()
+    tail = _run(xs[cut * C:], k, C, "auto", gpu, history=hist)
+    if dtype == "f32":
+        assert_f32_close(tail, full[cut * C:], f"k={k} C={C} history")
+    else:
+        assert np.array_equal(tail, full[cut * C:]), f"k={k} C={C} history"
+
+
 def _wide_windows(dsp, C, dt=None):
     """Windows around every shape change of the wide tile (halo rows, tile
     length, the last window it takes) and a few inside each range."""

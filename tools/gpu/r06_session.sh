@@ -4,6 +4,9 @@
 #   tools/gpu/r06_session.sh <tag> <step> [<step> ...]
 # steps: counters fullsize_new gloo2 ab_i16_mono ab_i16_stereo ab_i16_c4 ab_i16_c8
 #        gpu_tests bench bench_all
+#        wab:<k>:<C>:<f32|i16>:<mode>  tools/tune/wide_ab at 2^30 samples, 6 rounds (mode: - self selfhs hs)
+#        pt:<file>:<-k expression>     pytest -m gpu on one test file, selected by -k
+#        b:<workload>                  one bench.py line (--steps 20 --warmup 5, no CPU baseline)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:?tag}; shift
@@ -31,6 +34,13 @@ for s in "$@"; do
     gpu_tests) run gpu_tests 1100 $PYT --timeout 300 -m gpu tests/ ;;
     bench) run bench 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench_all) run bench_all 900 python -u bench.py --steps 20 --warmup 5 --all-workloads --no-cpu-baseline ;;
+    wab:*) IFS=: read -r _ k c dt mode <<< "$s"
+           [ "$mode" = "-" ] && mode=""
+           run "wab_${dt}_c${c}_k${k}_${mode:-default}" 300 tools/tune/wide_ab 30 "$k" "$c" 6 0 "$dt" $mode ;;
+    pt:*) IFS=: read -r _ f expr <<< "$s"
+          run "pt_$(basename "$f" .py)_$(echo "$expr" | tr -c 'A-Za-z0-9' '_' | cut -c1-40)" 1000 \
+              $PYT --timeout 300 -m gpu "tests/$f" -k "$expr" ;;
+    b:*) w=${s#b:}; run "bench_$w" 200 python -u bench.py --workload "$w" --steps 20 --warmup 5 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -90,12 +90,13 @@ void addU(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D, size_
 
 // the wide look-ahead scan with the channel-per-lane in-tile scan (CH)
 template <typename T, typename A, int C, int Q, int WG, int F, int U, bool XG = false, int MW = 0>
-void addAC(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
+void addAC(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D, bool self = false) {
   constexpr int kNtA = kNtStore | kNtHalo;
   char name[80];
-  snprintf(name, sizeof name, "wahead chan Q%d %d F%d U%d D%d xg%d mw%d", Q, WG, F, U, D, (int)XG, MW);
+  snprintf(name, sizeof name, "wahead chan Q%d %d F%d U%d D%d xg%d mw%d%s", Q, WG, F, U, D, (int)XG, MW,
+           self ? " self" : "");
   vs.push_back({name, [=](hipStream_t s) {
-                  return launch_wide_ahead<T, A, C, Q, 1, WG, kNtA, 0, F, U, true, XG, MW>(sg, k, s, ws, D);
+                  return launch_wide_ahead<T, A, C, Q, 1, WG, kNtA, 0, F, U, true, XG, MW>(sg, k, s, ws, D, self);
                 }, {}});
 }
 
@@ -122,6 +123,38 @@ void add_hs(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   for (int D : {512, 768, 1024, 1536}) {
     addH<T, A, C, F, true, 2>(vs, sg, k, ws, D);
     addH<T, A, C, F, false, 2>(vs, sg, k, ws, D);
+  }
+}
+
+// round 6: the look-ahead scan's record forms against each other at one shape -- look-ahead
+// (phase A, D slots) or aggregate-first (self-published, no phase A), per-tile records, tiles of
+// U units x WG threads
+template <typename T, typename A, int C, int F, int U, int WG, bool HS = false, bool WREC = false>
+void addS(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D, bool self) {
+  constexpr bool RC = sizeof(T) == 4 && C == 1 && !HS;
+  constexpr int kNtA = kNtStore | kNtHalo;
+  char name[96];
+  snprintf(name, sizeof name, "ahead%s U%d WG%d tile%d wrec=%d D%d%s", HS ? " hs" : "", U, WG, U * WG * F, (int)WREC,
+           D, self ? " self" : "");
+  vs.push_back({name, [=](hipStream_t s) {
+                  return launch_ahead_scan<T, A, C, F, U, kNtA, RC, true, WREC, 0, HS, false, WG>(sg, k, s, ws, D, self);
+                }, {}});
+}
+template <typename T, typename A, int C>
+void add_self(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, bool hs) {
+  constexpr int F = 16 / (C * (int)sizeof(T));
+  if (!hs) {
+    addS<T, A, C, F, 4, 256>(vs, sg, k, ws, C == 1 ? 512 : 768, false);
+    addS<T, A, C, F, 8, 256>(vs, sg, k, ws, 256, false);
+    addS<T, A, C, F, 4, 256>(vs, sg, k, ws, 512, true);
+    addS<T, A, C, F, 8, 256>(vs, sg, k, ws, 256, true);
+    addS<T, A, C, F, 4, 512>(vs, sg, k, ws, 512, true);
+    addS<T, A, C, F, 8, 512>(vs, sg, k, ws, 256, true);
+  } else {
+    addS<T, A, C, F, 4, 256, true, C == 1>(vs, sg, k, ws, 512, false);
+    addS<T, A, C, F, 4, 256, true>(vs, sg, k, ws, 512, true);
+    addS<T, A, C, F, 8, 256, true>(vs, sg, k, ws, 256, true);
+    addS<T, A, C, F, 4, 512, true>(vs, sg, k, ws, 512, true);
   }
 }
 
@@ -249,6 +282,10 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
       addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 512);
       addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 512);
       addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 768);
+      // aggregate-first (self-published records from the registers) against the look-ahead
+      addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 384, true);
+      addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 512, true);
+      addAC<T, A, C, 32, 128, 1, 8, true>(vs, sg, k, ws, 384, true);
     }
     return;
   }
@@ -288,7 +325,10 @@ int main(int argc, char** argv) {
   const int dist = argc > 5 ? atoi(argv[5]) : 1;
   const bool i16 = argc > 6 && std::string(argv[6]) == "i16";
   const bool hs = argc > 7 && std::string(argv[7]) == "hs";  // the Hillis-Steele look-ahead forms
-  const int algo = hs ? MAVG_ALGO_HILLIS : MAVG_ALGO_BLELLOCH;
+  // "self" / "selfhs": the record forms of the look-ahead scan (add_self), Blelloch / Hillis-Steele
+  const bool selfab = argc > 7 && (std::string(argv[7]) == "self" || std::string(argv[7]) == "selfhs");
+  const bool selfhs = argc > 7 && std::string(argv[7]) == "selfhs";
+  const int algo = hs || selfhs ? MAVG_ALGO_HILLIS : MAVG_ALGO_BLELLOCH;
   const int dt = i16 ? MAVG_I16 : MAVG_F32;
   const int eb = i16 ? 2 : 4;
   const int steps = 10;
@@ -315,7 +355,18 @@ int main(int argc, char** argv) {
                 }, {}});
   vs.push_back({"copy", [=](hipStream_t s) { return mavg_stream_copy(x, y, n * eb, s); }, {}});
   const Workspace w2{ws, ws2};
-  if (hs) {
+  if (selfab) {
+    switch (C * (i16 ? -1 : 1)) {
+      case 1: add_self<float, double, 1>(vs, sg, k, w2, selfhs); break;
+      case 2: add_self<float, double, 2>(vs, sg, k, w2, selfhs); break;
+      case -1: add_self<int16_t, int32_t, 1>(vs, sg, k, w2, selfhs); break;
+      case -2: add_self<int16_t, int32_t, 2>(vs, sg, k, w2, selfhs); break;
+      case 4: add_self<float, double, 4>(vs, sg, k, w2, selfhs); break;
+      case -4: add_self<int16_t, int32_t, 4>(vs, sg, k, w2, selfhs); break;
+      case -8: add_self<int16_t, int32_t, 8>(vs, sg, k, w2, selfhs); break;
+      default: fprintf(stderr, "self: f32 C=1/2/4, i16 C=1/2/4/8\n"); return 1;
+    }
+  } else if (hs) {
     if (C == 1 && !i16) add_hs<float, double, 1>(vs, sg, k, w2);
     else if (C == 2 && i16) add_hs<int16_t, int32_t, 2>(vs, sg, k, w2);
     else if (C == 1 && i16) add_hs<int16_t, int32_t, 1>(vs, sg, k, w2);
