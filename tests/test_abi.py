@@ -195,6 +195,20 @@ def test_plan_describes_launch_without_gpu():
     i16c8 = lambda k: dsp.plan(1 << 30, k, channels=8, dtype=dsp.I16)
     assert i16c8(1024).startswith("wide_tile<i16") and i16c8(2048).startswith("chan_tile<i16,acc=i32,C=8,Q=32")
     assert i16c8(44100).startswith("wide_ahead<i16,acc=i32,C=8,P=32") and ",ch=1,xg=1," in i16c8(44100)
+    # aggregate-first look-ahead records in 32-KiB tiles (round 6): int16 mono / stereo past a
+    # 16-KiB halo, int16 4 channels past 64 KiB, fp32 stereo past the wide tile's 32 KiB, short of
+    # the L2 reach (int16 mono: k <= 131072); fp32 mono and 8 channels keep their kernels
+    agg = lambda p: p.startswith("ahead_scan<") and " self=1 " in p and ",U=8," in p
+    i16 = lambda k, C: dsp.plan(1 << 30, k, channels=C, dtype=dsp.I16)
+    assert i16(8192, 1).startswith("tile_scan<") and agg(i16(8193, 1)) and agg(i16(131072, 1))
+    assert not agg(i16(131073, 1)) and i16(131073, 1).startswith("ahead_scan<")
+    assert i16(4096, 2).startswith("tile_scan<") and agg(i16(4097, 2)) and agg(i16(500_000, 2))
+    assert not agg(i16(600_000, 2))  # past the L2 reach: window-matched runs
+    assert i16(8192, 4).startswith("wide_ahead<") and agg(i16(8193, 4)) and agg(i16(100_000, 4))
+    assert dsp.plan(1 << 30, 4096, channels=2).startswith("wide_tile<") and agg(dsp.plan(1 << 30, 4097, channels=2))
+    assert not agg(dsp.plan(1 << 30, 300_000, channels=2)) and not agg(dsp.plan(1 << 30, 44100))
+    assert not agg(i16(44100, 8)) and not agg(dsp.plan(1 << 30, 44100, channels=4))
+    assert not agg(dsp.plan(1 << 30, 44100, channels=2, algo="hillis"))
     assert dsp.plan(3 << 28, 1024, channels=3).startswith("tile_scan<f32")  # 12-B frames: frame units
     assert dsp.plan(1 << 30, 1024, channels=2, algo="hillis").startswith("tile_scan<")
     # int16 keeps the register-staged tiles (bench.py's timing, tools/tune/ab_libs.py)
@@ -249,7 +263,7 @@ def test_workspace_only_for_ahead_scan():
     assert dsp.workspace_bytes(1 << 30, 8192, algo="blelloch_scalar") == 4 * tiles * 4 * 2 * 8 + 16
     assert dsp.plan(1 << 30, 8192, algo="hillis").startswith("ahead_scan<") and "hillis" in dsp.plan(
         1 << 30, 8192, algo="hillis")
-    # int16 keeps the 1024-thread tile up to ~47 KiB of halo
+    # int16 mono keeps the tiles up to 16 KiB of halo (past it: the aggregate-first look-ahead)
     assert dsp.workspace_bytes(1 << 30, 8192, dtype=dsp.I16) == 0
     n = 2 * 1_000_003
     st = (n // 2) // 1024     # int16 stereo, frame-unit tiles: one int32 word per (whole tile, channel)

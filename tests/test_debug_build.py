@@ -107,11 +107,17 @@ assert r["mismatches"] == 0, r
 # 8 fp32 channels: the wide tile (k <= 1024) and the look-ahead scan's 64-B units past it;
 # stereo fp32 with an odd window (the half-granule x[n-k] extraction)
 for C, k, kern in ((8, 1024, "chan_tile<"), (8, 5, "chan_tile<"), (8, 3000, "wide_ahead<"), (2, 1023, "wide_tile<"), (4, 7, "wide_tile<"),
-                   (4, 9000, "wide_ahead<"), (2, 20_000, "wide_ahead<")):
+                   (4, 9000, "wide_ahead<"), (2, 20_000, "ahead_scan<")):
     assert dsp.plan(300_007 * C, k, C, dsp.F32).startswith(kern), (C, k)
     xf = oracle.synth_f32(300_007 * C, seed=8, dist=1)
     y, rf = run(xf, k, C, "auto").astype(np.float64), oracle.mavg_f32(xf, k, C).astype(np.float64)
     assert (np.abs(y - rf) <= 1e-5 * np.maximum(np.abs(rf), 1e-30)).all(), (C, k)
+# int16 mono / stereo / 4 channels past the tiles: aggregate-first records in 32-KiB tiles (round 6)
+for C, k in ((1, 20_000), (2, 44_100), (4, 9_000)):
+    p = dsp.plan(100_003 * C, k, C, dsp.I16)
+    assert p.startswith("ahead_scan<i16") and "self=1" in p and "U=8" in p, p
+    xs = oracle.synth_i16(100_003 * C, seed=k)
+    assert np.array_equal(run(xs, k, C, "auto"), oracle.mavg_i16(xs, k, C)), (C, k)
 # int16 with 8 channels: the dword-column (two channels per lane) chan tile and look-ahead
 for k, kern in ((2048, "chan_tile<i16"), (3000, "chan_tile<i16"), (20_000, "wide_ahead<i16")):
     assert dsp.plan(100_003 * 8, k, 8, dsp.I16).startswith(kern), k

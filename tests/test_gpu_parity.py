@@ -670,7 +670,10 @@ def test_wide_tile_every_window_edge(oracle_mod, gpu, C):
         r = oracle_mod.check_synth_exact(_run(x, k, C, "blelloch", gpu), k, C, seed=k, dist=2, rtol=RTOL)
         assert r["mismatches"] == 0 and r["max_cond"] <= 2.0 ** -24 + 1e-9, (k, plan, r)
     tile = "chan_tile<" if C == 8 else "wide_tile<"  # 8 channels: one channel per lane
-    assert any(p.startswith(tile) for p in seen) and any(p.startswith("wide_ahead<") for p in seen), seen
+    # past the wide tile: stereo takes the aggregate-first unit look-ahead (round 6), 4 / 8 channels
+    # the wide look-ahead
+    ahead = "ahead_scan<" if C == 2 else "wide_ahead<"
+    assert any(p.startswith(tile) for p in seen) and any(p.startswith(ahead) for p in seen), seen
 
 
 @pytest.mark.parametrize("C", [4, 8])
@@ -774,7 +777,9 @@ def test_f32_multichannel_long_windows_every_form(oracle_mod, gpu, C, k):
     import torch
     frames = 300_007
     plan = dsp.plan(frames * C, k, C, dsp.F32)
-    assert plan.startswith("wide_ahead<"), plan
+    # stereo: the aggregate-first unit look-ahead in 4096-frame tiles (round 6)
+    assert plan.startswith("ahead_scan<" if C == 2 else "wide_ahead<"), plan
+    assert C != 2 or ("self=1" in plan and "U=8" in plan), plan
     assert dsp.plan(frames * C, k, C, dsp.F32, "blelloch_scalar").startswith("ahead_scan<")
     x = oracle_mod.synth_f32(frames * C, seed=k, dist=2)
     r = oracle_mod.check_synth_exact(_run(x, k, C, "blelloch", gpu), k, C, seed=k, dist=2, rtol=RTOL)
@@ -789,11 +794,11 @@ def test_f32_multichannel_long_windows_every_form(oracle_mod, gpu, C, k):
     assert_f32_close(_run(x, k, C, "blelloch_scalar", gpu), ref, f"k={k} scalar")
 
 
-@pytest.mark.parametrize("C,k", [(2, 4097), (2, 44_100), (4, 3585), (4, 20_000), (8, 2049), (8, 44_100),
-                                 (8, 700_000)])
+@pytest.mark.parametrize("C,k", [(2, 300_000), (4, 3585), (4, 20_000), (8, 2049), (8, 44_100), (8, 700_000)])
 def test_wide_ahead_bitwise_whatever_the_schedule(oracle_mod, gpu, C, k):
     """Multi-channel fp32 windows past the wide tile run the wide look-ahead
-    scan: rounding data (dist 2) within the bar against the exact window sums,
+    scan (stereo: past the L2 reach; shorter stereo windows take the
+    aggregate-first unit look-ahead, test_aggregate_first_records): rounding data (dist 2) within the bar against the exact window sums,
     and bitwise the same output when every record is recomputed by its
     consumer (spin 0), under the one-pass (slots 0) and minimal look-ahead
     schedules (the debug build's schedule hook) as under the release build's
@@ -1034,14 +1039,15 @@ import oracle
 import digital_signal_processsing_amd as dsp
 oracle.build()
 n, k, C = 2 * 300_007, 10_000, 2
-plan = dsp.plan(n, k, C, dsp.I16)
+# the reference block size 1024 (the tuned dispatch takes the look-ahead scan at this window)
+plan = dsp.plan(n, k, C, dsp.I16, block_size=1024)
 assert "block=1024" in plan and int(plan.split("lds=")[1].split()[0]) > 64 * 1024, plan
 x = oracle.synth_i16(n, seed=91)
 ref = oracle.mavg_i16(x, k, C)
 out = {}
 def launch(tag):
     torch.cuda.set_device(0)  # hipSetDevice re-issued on a thread that has not launched yet
-    y = dsp.moving_average(torch.from_numpy(x).to("cuda:0"), k, channels=C)
+    y = dsp.moving_average(torch.from_numpy(x).to("cuda:0"), k, channels=C, block_size=1024)
     torch.cuda.synchronize()
     out[tag] = bool(np.array_equal(y.cpu().numpy(), ref))
 for tag in ("first", "second"):
@@ -1054,7 +1060,7 @@ print("dyn lds ok")
 
 def test_dynamic_lds_tile_from_fresh_threads(gpu):
     """The 1024-thread tile above the default 64 KiB dynamic-LDS limit (int16
-    stereo k=10000, 73 KiB), first launched from a fresh thread after
+    stereo k=10000 at the reference block size 1024, 73 KiB), first launched from a fresh thread after
     hipSetDevice(0) in a fresh process, then again from another thread: the
     limit is raised per (kernel, device) on the current device
     (mavg_launch.hpp raise_dyn_lds_limit), and both outputs match the oracle."""

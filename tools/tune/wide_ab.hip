@@ -247,7 +247,7 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   using A = int32_t;
   constexpr int VF = 16 / (2 * C);
   add_unit<T, A, C, VF>(vs, sg, k, ws);
-  if (k > 8192) {  // the look-ahead range
+  if (k > 8192 || (C == 8 && k > 3072)) {  // the look-ahead range (8 channels: past the chan tile)
     if constexpr (C == 1) {  // mono: per-wave records, D = 512 (the library's dispatch)
       addU<T, A, C, 8, 4, false, true, false>(vs, sg, k, ws, 512);
       // aggregate-first (self-published records) against the look-ahead
@@ -284,8 +284,11 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
       addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 768);
       // aggregate-first (self-published records from the registers) against the look-ahead
       addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 384, true);
-      addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 512, true);
-      addAC<T, A, C, 32, 128, 1, 8, true>(vs, sg, k, ws, 384, true);
+      // 4096-frame tiles (a window of 11 instead of 21): 512 threads, or 64 frames per lane
+      addAC<T, A, C, 32, 512, 1, 8, true>(vs, sg, k, ws, 384, true);
+      addAC<T, A, C, 32, 512, 1, 8, true>(vs, sg, k, ws, 384);
+      addAC<T, A, C, 64, 256, 1, 16, true>(vs, sg, k, ws, 384, true);
+      addAC<T, A, C, 64, 256, 1, 16, true>(vs, sg, k, ws, 384);
     }
     return;
   }
