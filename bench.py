@@ -63,6 +63,7 @@ WORKLOADS = {
     # record carry with the log-step in-tile scan), and very long windows
     "hillis_long": (1 << 30, 44100, 1, "f32", "hillis"),
     "long_1m": (1 << 30, 1_000_000, 1, "f32", "blelloch"),
+    "long_2m": (1 << 30, 2_000_000, 1, "f32", "blelloch"),
     "long_4m": (1 << 30, 4_000_000, 1, "f32", "blelloch"),
     # fp32 multi-channel frames: stereo (the fp32 form of the reference's WAV
     # harness layout and of its only vectorized scan, longlong2 frames), 4 and 8

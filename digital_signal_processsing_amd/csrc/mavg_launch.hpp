@@ -477,18 +477,37 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     if (agg_first_range<T, C>(k))
       return launch_ahead_scan<T, A, C, F, 8, kNtA, false, true, false, 0, false, false, WG>(sg, k, st, ws, 256, true);
   }
-  constexpr bool kU8 = !HS && U0 == 4 && F * C * (int)sizeof(T) == 16 &&
-                       ((sizeof(T) == 4 && C == 1) || (sizeof(T) == 2 && C == 2));
-  if constexpr (kU8) {
+  // Past the L2 reach (window-matched runs, remap mode G; round 6): fp32 mono and int16 mono /
+  // stereo in the same 32-KiB tiles without run totals up to 1024 tiles per window, with
+  // self-published records -- except int16 mono past k = 2^21, which keeps phase A.  There D
+  // only bounds the run length (G <= D/20; the records a carry reads are J periods old): 320,
+  // 960 for int16 stereo past 2^21.  Self-publication also takes phase A's prefetched tiles out of
+  // the XCD's L2, where they competed with x[n-k].  In-process A/B, 2^30 samples
+  // (profiles/r06_tuning/far/): fp32 mono k=6e5 0.685 -> 0.720, 1e6 0.675 -> 0.713, 2e6 0.675
+  // -> 0.702, 4e6 0.645 -> 0.664, 8e6 0.579 -> 0.578 (against the 8192-frame look-ahead);
+  // int16 mono 1.5e6 0.598 -> 0.665, 2.2e6 0.573 -> 0.650 (phase A), 4e6 0.527 -> 0.663 (phase A;
+  // self-published 0.602); int16 stereo 6e5 0.569 -> 0.720, 2e6 0.489 -> 0.691, 4e6 0.484 ->
+  // 0.652 (against the 8192-frame look-ahead with D = 256, i.e. G <= 12, and the run-total kernel).
+  constexpr bool kFar = !HS && U0 == 4 && F * C * (int)sizeof(T) == 16 && (C == 1 || (sizeof(T) == 2 && C == 2));
+  if constexpr (kFar) {
     constexpr int TF8 = WG * F * 8;
-    const bool u8 = sizeof(T) == 4 ? !self && ahead_past_l2(k, C, sizeof(T), TF8) && (long long)k <= kAheadU8MaxTiles * TF8
-                                   : !(ahead_past_l2(k, C, sizeof(T), TF) && (long long)k > 384LL * TF);
+    if (ahead_past_l2(k, C, sizeof(T), TF8) && (long long)k <= kAheadU8MaxTiles * TF8) {
+      const bool far_self = !(sizeof(T) == 2 && C == 1 && k > (1 << 21));
+      const int far_d = sizeof(T) == 2 && C == 2 && k > (1 << 21) ? 960 : 320;
+      return launch_ahead_scan<T, A, C, F, 8, kNtA, kRC, true, false, 0, false, false, WG>(sg, k, st, ws, far_d,
+                                                                                        far_self);
+    }
+  }
+  constexpr bool kU8 = !HS && U0 == 4 && F * C * (int)sizeof(T) == 16 && sizeof(T) == 2 && C == 2;
+  if constexpr (kU8) {
+    // (int16 stereo windows that reach here short of the run-total range: the reference block
+    // size's fallbacks; the tuned dispatch takes the tiles or the aggregate-first form)
+    const bool u8 = !(ahead_past_l2(k, C, sizeof(T), TF) && (long long)k > 384LL * TF);
     // phase A keeps the default policy: non-temporal phase-A loads (kNtPhaseA) measured +3-4 % in
     // the in-process tuner but -15 to -18 % in bench.py's timing (round 4, profiles/r04_tuning/u8/
     // nta_*, bench_timing_nta_*: k=4e6 0.620 -> 0.510, 2e6 0.652 -> 0.546, 1e6 0.660 -> 0.556)
     constexpr int kNt8 = kNtA;
-    if (u8) return launch_ahead_scan<T, A, C, F, 8, kNt8, kRC, true, false, 0, false, false, WG>(sg, k, st, ws,
-                                                                                              sizeof(T) == 4 ? 320 : 256);
+    if (u8) return launch_ahead_scan<T, A, C, F, 8, kNt8, kRC, true, false, 0, false, false, WG>(sg, k, st, ws, 256);
   }
   // per-wave records: mono only (instantiated for C = 1 alone)
   const bool wrec = C == 1 && (long long)k / TF + 1 <= 64;

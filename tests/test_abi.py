@@ -203,7 +203,16 @@ def test_plan_describes_launch_without_gpu():
     assert i16(8192, 1).startswith("tile_scan<") and agg(i16(8193, 1)) and agg(i16(131072, 1))
     assert not agg(i16(131073, 1)) and i16(131073, 1).startswith("ahead_scan<")
     assert i16(4096, 2).startswith("tile_scan<") and agg(i16(4097, 2)) and agg(i16(500_000, 2))
-    assert not agg(i16(600_000, 2))  # past the L2 reach: window-matched runs
+    # past the L2 reach: window-matched runs of the same tiles, self-published (int16 mono past
+    # k = 2^21: phase A), no run totals up to 1024 tiles per window
+    far = lambda p: p.startswith("ahead_scan<") and ",U=8," in p and " remap=1 " not in p and "runs=1" not in p
+    assert far(i16(600_000, 2)) and " self=1 " in i16(600_000, 2) and " ahead=320 " in i16(600_000, 2)
+    assert far(i16(4_000_000, 2)) and " self=1 " in i16(4_000_000, 2) and " ahead=960 " in i16(4_000_000, 2)
+    assert far(i16(1_500_000, 1)) and " self=1 " in i16(1_500_000, 1)
+    assert far(i16(4_000_000, 1)) and " self=1 " not in i16(4_000_000, 1)
+    for k in (600_000, 1_000_000, 4_000_000, 8_000_000):
+        assert far(dsp.plan(1 << 30, k)) and " self=1 " in dsp.plan(1 << 30, k), k
+    assert "runs=1" in dsp.plan(1 << 30, 9_000_000)  # past 1024 tiles: the run-total kernel
     assert i16(8192, 4).startswith("wide_ahead<") and agg(i16(8193, 4)) and agg(i16(100_000, 4))
     assert dsp.plan(1 << 30, 4096, channels=2).startswith("wide_tile<") and agg(dsp.plan(1 << 30, 4097, channels=2))
     assert not agg(dsp.plan(1 << 30, 300_000, channels=2)) and not agg(dsp.plan(1 << 30, 44100))

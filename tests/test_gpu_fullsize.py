@@ -30,6 +30,9 @@ CONFIGS = [
     ("i16_stereo_2p30_k1024", 1 << 30, 1024, 2, "i16", "blelloch"),  # the reference's stereo PCM layout
     ("long_1m_k1000000", 1 << 30, 1_000_000, 1, "f32", "blelloch"),  # window-matched runs
     ("long_4m_k4000000", 1 << 30, 4_000_000, 1, "f32", "blelloch"),  # window-matched runs, 8192-frame tiles
+    # int16 past the L2 reach: self-published records in window-matched runs (stereo), phase A (mono)
+    ("i16_stereo_2p30_k2000000", 1 << 30, 2_000_000, 2, "i16", "blelloch"),
+    ("i16_mono_2p30_k4000000", 1 << 30, 4_000_000, 1, "i16", "blelloch"),
     ("f32_stereo_2p30_k1024", 1 << 30, 1024, 2, "f32", "blelloch"),  # fp32 form of the stereo harness layout
     ("f32_c4_2p30_k1024", 1 << 30, 1024, 4, "f32", "blelloch"),
     ("f32_c8_2p30_k1024", 1 << 30, 1024, 8, "f32", "blelloch"),

@@ -489,7 +489,8 @@ def _with_schedule(sched, fn, debug=False):
 @pytest.mark.parametrize("dtype,C,k", [("f32", 1, 20_000), ("f32", 3, 9_000), ("i16", 2, 44_100),
                                        ("i16", 1, 100_000), ("f32", 1, 300_000), ("f32", 2, 600_000),
                                        ("f32", 1, 1_100_000), ("i16", 1, 2_200_000),
-                                       ("i16", 8, 5_000), ("i16", 8, 44_100), ("i16", 4, 44_100)])
+                                       ("i16", 8, 5_000), ("i16", 8, 44_100), ("i16", 4, 44_100),
+                                       ("i16", 2, 600_000), ("i16", 1, 1_500_000)])
 def test_ahead_records_bitwise_whatever_the_schedule(oracle_mod, gpu, dtype, C, k):
     """Every record is the same bits whether its producer published it (look-
     ahead D slots, head duty, own tile) or the consumer recomputed it after a

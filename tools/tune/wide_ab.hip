@@ -143,6 +143,14 @@ void addS(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D, bool 
 template <typename T, typename A, int C>
 void add_self(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, bool hs) {
   constexpr int F = 16 / (C * (int)sizeof(T));
+  if (!hs && k > 500000) {  // past the L2 reach (window-matched runs: D also sets the run length G)
+    addS<T, A, C, F, 8, 256>(vs, sg, k, ws, 320, false);
+    addS<T, A, C, F, 8, 256>(vs, sg, k, ws, 320, true);
+    addS<T, A, C, F, 8, 256>(vs, sg, k, ws, 640, true);
+    addS<T, A, C, F, 8, 256>(vs, sg, k, ws, 960, true);
+    addS<T, A, C, F, 4, 256>(vs, sg, k, ws, 1024, true);
+    return;
+  }
   if (!hs) {
     addS<T, A, C, F, 4, 256>(vs, sg, k, ws, C == 1 ? 512 : 768, false);
     addS<T, A, C, F, 8, 256>(vs, sg, k, ws, 256, false);
