@@ -64,16 +64,19 @@ def test_plans_pick_window_matched_runs_past_the_l2_reach():
     plan = lambda k, C, dt: dsp.plan(1 << 30, k, C, dt)
     remap = lambda k, C, dt: int(re.search(r"remap=(\d+)", plan(k, C, dt)).group(1))
     assert remap(44_100, 1, dsp.F32) == 1 and remap(300_000, 1, dsp.F32) == 1
-    # fp32 mono and int16 stereo: 8192-frame tiles (U=8, D=320 / 256 slots) short of the run
-    # totals (fp32: past 1024 tiles; int16 stereo: the 4096-frame run-total kernel past 384)
+    # 32-KiB tiles (U=8) without run totals up to 1024 tiles per window (round 6): fp32 mono and
+    # int16 stereo 8192-frame tiles, int16 mono 16384; D (320; int16 stereo past 2^21: 960) sets the
+    # run length; past 1024 tiles the 4096-frame run-total kernel
     for k, C, dt, tf, ahead, runs in ((600_000, 1, dsp.F32, 8192, 320, False),
                                       (1_000_000, 1, dsp.F32, 8192, 320, False),
                                       (4_000_000, 1, dsp.F32, 8192, 320, False),
                                       (10_000_000, 1, dsp.F32, 4096, 1024, True),
-                                      (1_000_000, 2, dsp.I16, 8192, 256, False),
-                                      (2_000_000, 2, dsp.I16, 4096, 768, True),
-                                      (1_500_000, 1, dsp.I16, 8192, 1024, False),
-                                      (4_000_000, 1, dsp.I16, 8192, 1024, True)):
+                                      (1_000_000, 2, dsp.I16, 8192, 320, False),
+                                      (4_000_000, 2, dsp.I16, 8192, 960, False),
+                                      (10_000_000, 2, dsp.I16, 4096, 768, True),
+                                      (1_500_000, 1, dsp.I16, 16384, 320, False),
+                                      (4_000_000, 1, dsp.I16, 16384, 320, False),
+                                      (20_000_000, 1, dsp.I16, 8192, 1024, True)):
         p = plan(k, C, dt)
         assert "tile_frames=%d " % tf in p and " ahead=%d " % ahead in p, (k, C, p)
         assert remap(k, C, dt) == run_length(k, tf, ahead), (k, C)
