@@ -492,7 +492,11 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   if constexpr (kFar) {
     constexpr int TF8 = WG * F * 8;
     if (ahead_past_l2(k, C, sizeof(T), TF8) && (long long)k <= kAheadU8MaxTiles * TF8) {
+#ifdef MAVG_VARIANT_FAR_NOSELF  // round-6 A/B only (tools/tune/ab_libs.py): phase A past the L2 reach
+      const bool far_self = false;
+#else
       const bool far_self = !(sizeof(T) == 2 && C == 1 && k > (1 << 21));
+#endif
       const int far_d = sizeof(T) == 2 && C == 2 && k > (1 << 21) ? 960 : 320;
       return launch_ahead_scan<T, A, C, F, 8, kNtA, kRC, true, false, 0, false, false, WG>(sg, k, st, ws, far_d,
                                                                                         far_self);
@@ -615,6 +619,78 @@ int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   }
   hipLaunchKernelGGL((wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH, XG, MW>), dim3((unsigned)ntiles), dim3(WG), lds,
                      st, p);
+  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
+}
+
+// paired look-ahead scan (mavg_pair.hpp): the halo-only channel-per-lane look-ahead with two
+// consecutive tiles per workgroup (tile t + 1 chains tile t's carry); windows short of the L2
+// reach (remap mode 1), 16- or 32-B frames, 16-B-aligned views.  The records and their
+// workspace are the one-tile kernel's (per tile, per virtual slot); the grid is 8 workgroups per
+// pair of run positions.
+template <typename T, typename A, int C, int P, int WG, int NT, int DV, int U>
+int launch_pair_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
+  constexpr int NW = WG / 64;
+  constexpr int EPG = 16 / (int)sizeof(T);
+  constexpr int CL = C * (int)sizeof(T) / 4;
+  constexpr int TF = NW * (64 / CL) * P;
+  static_assert(TF == WG * U, "F = 1 record units");
+  constexpr int TG = TF * C / EPG;
+  using SA = typename ScanAcc<T, A>::type;
+  const long long nframes = sg.nframes;
+  if (ahead_past_l2(k, C, sizeof(T), TF) || (long long)k < TF) return MAVG_ERR_UNSUPPORTED;
+  ahead &= ~7;
+  int spin = kAheadSpin;
+#ifdef MAVG_TEST_HOOKS
+  {
+    const int t = g_test_ahead_slots.load(std::memory_order_relaxed);
+    if (t >= 0) ahead = t & ~7;
+  }
+  {
+    const int t = g_test_ahead_spin.load(std::memory_order_relaxed);
+    if (t >= 0) spin = t;
+  }
+#endif
+  const long long ntiles = (nframes + TF - 1) / TF;
+  const long long nfull = nframes / TF;
+  if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  const long long q8 = (ntiles + 7) / 8;               // run positions of the longest run
+  const long long grid = 8 * ((q8 + 1) / 2);           // a workgroup per pair of positions per XCD
+  const size_t need = ahead_granule_bytes<T, A, C, 1, U>(nfull);
+  const size_t lds = (size_t)2 * (TG + 1) * 16 + (size_t)(NW * C + C) * sizeof(A) + (size_t)(2 + 6) * NW * C * sizeof(SA);
+  if (lds > 64 * 1024) return MAVG_ERR_UNSUPPORTED;
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text),
+             "pair_ahead<%s,acc=%s,C=%d,P=%d,nt=%d,dv=%d,FU=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
+             "ahead=%d remap=1 tiles=%lld ws=%zu",
+             type_name<T>(), type_name<A>(), C, P, NT, DV, U, grid, WG, lds, TF, ahead, ntiles, need);
+    g_plan->ws_bytes = need;
+    return MAVG_OK;
+  }
+  if (ws.ptr == nullptr || ws.bytes < need) return MAVG_ERR_WORKSPACE;
+  if ((reinterpret_cast<uintptr_t>(ws.ptr) & 15u) != 0) return MAVG_ERR_MISALIGNED;
+  if (hipMemsetAsync(ws.ptr, 0, need, st) != hipSuccess) return MAVG_ERR_HIP;
+  AheadParams p{};
+  p.in = sg.in;
+  p.out = sg.out;
+  p.hist = sg.hist;
+  p.nframes = nframes;
+  p.pre = sg.pre;
+  p.eio = 0;
+  p.nfull = nfull;
+  p.k = k;
+  p.o = make_out_params(k);
+  p.halo_units = k;
+  p.xk_off = 0;
+  p.xcd_remap = 1;
+  p.runs_done = 0;
+  p.ahead = ahead;
+  p.head = (int)std::min<long long>((long long)k / TF, nfull);
+  p.spin = spin;
+  p.self = 0;
+  p.gran = static_cast<unsigned long long*>(ws.ptr);
+  p.runs = nullptr;
+  p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
+  hipLaunchKernelGGL((pair_ahead_kernel<T, A, C, P, WG, NT, DV, U>), dim3((unsigned)grid), dim3(WG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 

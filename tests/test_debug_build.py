@@ -71,20 +71,23 @@ assert np.array_equal(run(xs, 12_000, 2, "blelloch"), oracle.mavg_i16(xs, 12_000
 assert np.array_equal(run(xs, 70_000, 2, "hillis"), oracle.mavg_i16(xs, 70_000, 2))
 # window-matched runs with run totals (k > 384 tiles; run_total's checks and,
 # with spin 0, the consumers' recompute of every record and run total)
-# (int16 stereo: fp32 mono takes 8192-frame tiles without run totals up to 1024 tiles)
+# (round 6: 16-B-unit int16 stereo takes 8192-frame tiles with self-published records and no run
+# totals up to 1024 tiles, so the run-total kernel is reached through the frame-unit form here)
 frames = 4096 * 620 + 5
-plan = dsp.plan(frames * 2, 1_600_000, 2, dsp.I16)
-assert plan.startswith("ahead_scan<") and "runs=1" in plan and " remap=1 " not in plan, plan
 xs = oracle.synth_i16(frames * 2, seed=6)
-y0 = run(xs, 1_600_000, 2, "auto")
-assert np.array_equal(y0, oracle.mavg_i16(xs, 1_600_000, 2))
+ref = oracle.mavg_i16(xs, 1_600_000, 2)
 lib = _lib.load()
-lib.mavg_test_ahead_schedule(-1, 0)
-try:
-    y1 = run(xs, 1_600_000, 2, "auto")
-finally:
-    lib.mavg_test_ahead_schedule(-1, -1)
-assert np.array_equal(y0, y1)
+for algo, want in (("blelloch_scalar", "runs=1"), ("auto", "self=1")):
+    plan = dsp.plan(frames * 2, 1_600_000, 2, dsp.I16, algo)
+    assert plan.startswith("ahead_scan<") and want in plan and " remap=1 " not in plan, plan
+    y0 = run(xs, 1_600_000, 2, algo)
+    assert np.array_equal(y0, ref), algo
+    lib.mavg_test_ahead_schedule(-1, 0)
+    try:
+        y1 = run(xs, 1_600_000, 2, algo)
+    finally:
+        lib.mavg_test_ahead_schedule(-1, -1)
+    assert np.array_equal(y0, y1), algo
 # fp32 mono 8192-frame tiles with window-matched runs (k = 10^6), recomputed records too
 frames = 8192 * 200 + 5
 plan = dsp.plan(frames, 1_000_000, 1, dsp.F32)

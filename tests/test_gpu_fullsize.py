@@ -51,6 +51,12 @@ CONFIGS = [
     ("i16_c8_2p30_k44100", 1 << 30, 44100, 8, "i16", "blelloch"),
     # the int16 dword-column chan tile (C = 8, 2048 <= k <= 3072) at full size
     ("i16_c8_2p30_k2048", 1 << 30, 2048, 8, "i16", "blelloch"),
+    # the chunk-form wide look-ahead (fp32 stereo past the L2 reach, int16 8 channels past int32
+    # sums) with a partial window (k mod tile != 0): the r05ad development build zeroed that part
+    # of the carry in this form, which the k = 44100 configs above no longer
+    # reach since those windows take the aggregate-first look-ahead
+    ("f32_stereo_2p30_k300001", 1 << 30, 300_001, 2, "f32", "blelloch"),
+    ("i16_c8_2p30_k70001", 1 << 30, 70_001, 8, "i16", "blelloch"),
 ]
 
 

@@ -5,7 +5,7 @@
 // checked against the library's (|dy| <= 1e-6 |y|, fp64 sums in another order).
 //
 // build: make -C tools/tune wide_ab
-// run:   tools/tune/wide_ab <log2n> <k> <C> [rounds] [dist] [f32|i16] [hs]
+// run:   tools/tune/wide_ab <log2n> <k> <C> [rounds] [dist] [f32|i16] [hs|self|selfhs|pair]
 // A copy of this file built against another tree's headers (round 5's wide_ab_prev / _cand /
 // _r04) compares that tree's kernels with this library's: the library is linked -Bsymbolic, so
 // its launches keep its own kernel code even where the template instances share a name.
@@ -163,6 +163,32 @@ void add_self(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, bool hs)
     addS<T, A, C, F, 4, 256, true>(vs, sg, k, ws, 512, true);
     addS<T, A, C, F, 8, 256, true>(vs, sg, k, ws, 256, true);
     addS<T, A, C, F, 4, 512, true>(vs, sg, k, ws, 512, true);
+  }
+}
+
+// round 6: the paired look-ahead (mavg_pair.hpp, two consecutive tiles per workgroup) against the
+// one-tile halo-only channel-per-lane look-ahead at the same tile shape
+template <typename T, typename A, int C, int Q, int WG, int U>
+void addP(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
+  constexpr int kNtA = kNtStore | kNtHalo;
+  char name[80];
+  snprintf(name, sizeof name, "pair chan Q%d %d U%d D%d", Q, WG, U, D);
+  vs.push_back({name, [=](hipStream_t s) { return launch_pair_ahead<T, A, C, Q, WG, kNtA, 0, U>(sg, k, s, ws, D); }, {}});
+}
+template <typename T, typename A, int C>
+void add_pair(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
+  if constexpr (sizeof(T) == 4 && C == 4) {
+    addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 768);
+    for (int D : {384, 768, 1024, 1536}) addP<T, A, C, 16, 256, 4>(vs, sg, k, ws, D);
+    addP<T, A, C, 8, 256, 2>(vs, sg, k, ws, 1536);
+  } else if constexpr (sizeof(T) == 4 && C == 8) {
+    addAC<T, A, C, 32, 256, 1, 4, true>(vs, sg, k, ws, 384);
+    addAC<T, A, C, 16, 256, 1, 2, true>(vs, sg, k, ws, 768);
+    for (int D : {384, 768, 1536}) addP<T, A, C, 16, 256, 2>(vs, sg, k, ws, D);
+  } else if constexpr (sizeof(T) == 2 && C == 8) {
+    addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 384);
+    addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 768);
+    for (int D : {384, 768, 1536}) addP<T, A, C, 16, 256, 4>(vs, sg, k, ws, D);
   }
 }
 
@@ -339,6 +365,7 @@ int main(int argc, char** argv) {
   // "self" / "selfhs": the record forms of the look-ahead scan (add_self), Blelloch / Hillis-Steele
   const bool selfab = argc > 7 && (std::string(argv[7]) == "self" || std::string(argv[7]) == "selfhs");
   const bool selfhs = argc > 7 && std::string(argv[7]) == "selfhs";
+  const bool pairab = argc > 7 && std::string(argv[7]) == "pair";  // the paired look-ahead (add_pair)
   const int algo = hs || selfhs ? MAVG_ALGO_HILLIS : MAVG_ALGO_BLELLOCH;
   const int dt = i16 ? MAVG_I16 : MAVG_F32;
   const int eb = i16 ? 2 : 4;
@@ -366,7 +393,14 @@ int main(int argc, char** argv) {
                 }, {}});
   vs.push_back({"copy", [=](hipStream_t s) { return mavg_stream_copy(x, y, n * eb, s); }, {}});
   const Workspace w2{ws, ws2};
-  if (selfab) {
+  if (pairab) {
+    switch (C * (i16 ? -1 : 1)) {
+      case 4: add_pair<float, double, 4>(vs, sg, k, w2); break;
+      case 8: add_pair<float, double, 8>(vs, sg, k, w2); break;
+      case -8: add_pair<int16_t, int32_t, 8>(vs, sg, k, w2); break;
+      default: fprintf(stderr, "pair: f32 C=4/8, i16 C=8\n"); return 1;
+    }
+  } else if (selfab) {
     switch (C * (i16 ? -1 : 1)) {
       case 1: add_self<float, double, 1>(vs, sg, k, w2, selfhs); break;
       case 2: add_self<float, double, 2>(vs, sg, k, w2, selfhs); break;
