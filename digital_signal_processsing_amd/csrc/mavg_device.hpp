@@ -56,6 +56,30 @@ __device__ __forceinline__ int64_t dpp(int64_t v) {
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+// 4 x 4 dword transpose inside each lane quad (lanes 4j .. 4j + 3), two DPP quad_perm stages:
+// on entry lane q holds a[e] = element (q, e), on exit a[f] = element (f, q).  Stage s (1, 2)
+// swaps the off-diagonal halves of the 2s x 2s blocks: per pair (e, e | s) a lane sends the value
+// its partner q ^ s keeps and takes the partner's (one cndmask, one DPP move, one cndmask).
+// (round 6: 16-B frame loads turned into the channel-per-lane columns, mavg_wide.hpp XL)
+__device__ __forceinline__ void quad_transpose4(uint32_t (&a)[4], int q) {
+#pragma unroll
+  for (int s = 1; s <= 2; s <<= 1) {
+    const bool hi_lane = (q & s) != 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (e & s) continue;
+      // value selects only (a select of the element to write made the compiler index the array
+      // through scratch)
+      const uint32_t lo = a[e], hi = a[e | s];
+      const uint32_t send = hi_lane ? lo : hi;
+      const uint32_t got = s == 1 ? (uint32_t)dpp<0xB1, 0xf, 0xf>((int32_t)send)    // quad_perm [1,0,3,2]
+                                  : (uint32_t)dpp<0x4E, 0xf, 0xf>((int32_t)send);   // quad_perm [2,3,0,1]
+      a[e] = hi_lane ? got : lo;
+      a[e | s] = hi_lane ? hi : got;
+    }
+  }
+}
+
 // Inclusive scan across the 64 lanes of a wave: Kogge-Stone inside each
 // 16-lane row (row_shr 1,2,4,8) then row_bcast:15 / row_bcast:31 to carry
 // row totals across rows -- 6 DPP steps, no LDS.

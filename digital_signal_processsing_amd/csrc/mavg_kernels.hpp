@@ -19,8 +19,6 @@
 //                      whole-tile records that tiles D slots ahead published
 //                      inside the launch; windows past the LDS-staged halo,
 //                      both flavours (Blelloch and Hillis-Steele in-tile scans).
-//   mavg_pair.hpp      pair_ahead_kernel: the halo-only channel-per-lane
-//                      look-ahead with two consecutive tiles per workgroup.
 //   mavg_direct.hpp    direct_kernel: small windows summed directly from LDS
 //                      (replaces profilable_sm_*.cu).
 //   mavg_misc.hpp      naive_kernel (profilable_parallel_averager.cu:14-23)
@@ -39,6 +37,5 @@
 #include "mavg_direct.hpp"
 #include "mavg_lookback.hpp"
 #include "mavg_misc.hpp"
-#include "mavg_pair.hpp"
 #include "mavg_tile.hpp"
 #include "mavg_wide.hpp"

@@ -196,7 +196,9 @@ int launch_wide_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
 // in-place output form (chan_tile_kernel IP).  In-process (profiles/r05_tuning/wide/ip_*): fp32
 // C = 4 k=2048 0.737 -> 0.756; fp32 C = 8 k=1024 0.750 -> 0.746 and int16 C = 8 k=2048 0.649 ->
 // 0.485 (170 VGPRs, 2 workgroups per CU), so only fp32 C = 4 asks for it
-template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false, bool IPOK = false>
+// XL: x as 16-B frame loads plus quad transposes (mavg_wide.hpp xl_load; XG with 16-B frames)
+template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false, bool IPOK = false,
+          int XL = 0>
 int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {
   constexpr int EPG = 16 / (int)sizeof(T);
   constexpr int NW = WG / 64;
@@ -214,8 +216,9 @@ int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
   const bool ip = XG && IPOK && Hg * EPG == (long long)k * C;  // staged halo frames Hg EPG / C == k
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "chan_tile<%s,acc=%s,C=%d,Q=%d,nt=%d,dv=%d%s%s> grid=%lld block=%d lds=%zu tile_frames=%d remap=%d",
-             type_name<T>(), type_name<A>(), C, Q, NT, DV, XG ? ",xg=1" : "", ip ? ",ip=1" : "", ntiles, WG, lds, TF,
+             "chan_tile<%s,acc=%s,C=%d,Q=%d,nt=%d,dv=%d%s%s%s> grid=%lld block=%d lds=%zu tile_frames=%d remap=%d",
+             type_name<T>(), type_name<A>(), C, Q, NT, DV, XG ? ",xg=1" : "", ip ? ",ip=1" : "", XL ? ",xl=1" : "",
+             ntiles, WG, lds, TF,
              xcd_remap);
     return MAVG_OK;
   }
@@ -234,10 +237,10 @@ int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
   auto launch = [&](auto ipc) -> int {
     constexpr bool IP = decltype(ipc)::value;
     if (lds > 64 * 1024) {
-      const int s = raise_dyn_lds_limit<&chan_tile_kernel<T, A, C, Q, WG, NT, DV, XG, IP>>(80 * 1024);
+      const int s = raise_dyn_lds_limit<&chan_tile_kernel<T, A, C, Q, WG, NT, DV, XG, IP, XL>>(80 * 1024);
       if (s != MAVG_OK) return s;
     }
-    hipLaunchKernelGGL((chan_tile_kernel<T, A, C, Q, WG, NT, DV, XG, IP>), dim3((unsigned)ntiles), dim3(WG), lds, st, p);
+    hipLaunchKernelGGL((chan_tile_kernel<T, A, C, Q, WG, NT, DV, XG, IP, XL>), dim3((unsigned)ntiles), dim3(WG), lds, st, p);
     return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
   };
   if constexpr (XG && IPOK) {
@@ -477,26 +480,21 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     if (agg_first_range<T, C>(k))
       return launch_ahead_scan<T, A, C, F, 8, kNtA, false, true, false, 0, false, false, WG>(sg, k, st, ws, 256, true);
   }
-  // Past the L2 reach (window-matched runs, remap mode G; round 6): fp32 mono and int16 mono /
-  // stereo in the same 32-KiB tiles without run totals up to 1024 tiles per window, with
-  // self-published records -- except int16 mono past k = 2^21, which keeps phase A.  There D
+  // Past the L2 reach (window-matched runs, remap mode G): fp32 mono and int16 mono / stereo in
+  // the same 32-KiB tiles without run totals up to 1024 tiles per window.  Round 6: int16 with
+  // self-published records (int16 mono only up to k = 2^21), fp32 mono keeping phase A.  There D
   // only bounds the run length (G <= D/20; the records a carry reads are J periods old): 320,
-  // 960 for int16 stereo past 2^21.  Self-publication also takes phase A's prefetched tiles out of
-  // the XCD's L2, where they competed with x[n-k].  In-process A/B, 2^30 samples
-  // (profiles/r06_tuning/far/): fp32 mono k=6e5 0.685 -> 0.720, 1e6 0.675 -> 0.713, 2e6 0.675
-  // -> 0.702, 4e6 0.645 -> 0.664, 8e6 0.579 -> 0.578 (against the 8192-frame look-ahead);
-  // int16 mono 1.5e6 0.598 -> 0.665, 2.2e6 0.573 -> 0.650 (phase A), 4e6 0.527 -> 0.663 (phase A;
-  // self-published 0.602); int16 stereo 6e5 0.569 -> 0.720, 2e6 0.489 -> 0.691, 4e6 0.484 ->
-  // 0.652 (against the 8192-frame look-ahead with D = 256, i.e. G <= 12, and the run-total kernel).
+  // 960 for int16 stereo past 2^21.  The in-process tuner favoured self-publication for fp32 too
+  // (k=1e6 0.675 -> 0.713, 4e6 0.645 -> 0.664) but bench.py's own timing did not: the release
+  // library against a phase-A build in bench.py's environment (tools/tune/ab_libs.py,
+  // tools/gpu/r06_far_ab.sh, profiles/r06_tuning/far/), self-published vs phase A: fp32 mono
+  // k=6e5 0.673 vs 0.692, 1e6 0.674 vs 0.684, 2e6 0.662 vs 0.673, 4e6 0.570 vs 0.639; int16 mono
+  // 1.5e6 0.634 vs 0.605, stereo 6e5 0.608 vs 0.584, 2e6 0.599 vs 0.577 (outputs bitwise equal).
   constexpr bool kFar = !HS && U0 == 4 && F * C * (int)sizeof(T) == 16 && (C == 1 || (sizeof(T) == 2 && C == 2));
   if constexpr (kFar) {
     constexpr int TF8 = WG * F * 8;
     if (ahead_past_l2(k, C, sizeof(T), TF8) && (long long)k <= kAheadU8MaxTiles * TF8) {
-#ifdef MAVG_VARIANT_FAR_NOSELF  // round-6 A/B only (tools/tune/ab_libs.py): phase A past the L2 reach
-      const bool far_self = false;
-#else
-      const bool far_self = !(sizeof(T) == 2 && C == 1 && k > (1 << 21));
-#endif
+      const bool far_self = sizeof(T) == 2 && !(C == 1 && k > (1 << 21));
       const int far_d = sizeof(T) == 2 && C == 2 && k > (1 << 21) ? 960 : 320;
       return launch_ahead_scan<T, A, C, F, 8, kNtA, kRC, true, false, 0, false, false, WG>(sg, k, st, ws, far_d,
                                                                                         far_self);
@@ -539,9 +537,10 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
 // in-tile scan (P-frame chunks x UW rows); 16-B-aligned views only.
 // self: aggregate-first (self-published) records, the int16 halo-only CH form only (wide_ahead_kernel)
 template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false,
-          bool XG = false, int MW = 0>
+          bool XG = false, int MW = 0, int XL = 0>
 int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead, bool self = false) {
-  if (self && !(CH && XG && std::is_integral<T>::value)) return MAVG_ERR_UNSUPPORTED;
+  // (self + XL: the self-published record would be summed before the quad transposes)
+  if (self && !(CH && XG && std::is_integral<T>::value && XL == 0)) return MAVG_ERR_UNSUPPORTED;
   constexpr int NW = WG / 64;
   constexpr int EPG = 16 / (int)sizeof(T);
   constexpr int CL = C * (int)sizeof(T) / 4 > 0 ? C * (int)sizeof(T) / 4 : 1;  // CH: dword columns per frame
@@ -579,9 +578,9 @@ int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   if (lds > 80 * 1024) return MAVG_ERR_UNSUPPORTED;
   if (g_plan) {
     snprintf(g_plan->text, sizeof(g_plan->text),
-             "wide_ahead<%s,acc=%s,C=%d,P=%d,U=%d,nt=%d,dv=%d,F=%d,FU=%d%s%s,mw=%d> grid=%lld block=%d lds=%zu "
+             "wide_ahead<%s,acc=%s,C=%d,P=%d,U=%d,nt=%d,dv=%d,F=%d,FU=%d%s%s,mw=%d,xl=%d> grid=%lld block=%d lds=%zu "
              "tile_frames=%d ahead=%d remap=%d%s ws=%zu",
-             type_name<T>(), type_name<A>(), C, P, UW, NT, DV, F, U, CH ? ",ch=1" : "", XG ? ",xg=1" : "", MW, ntiles,
+             type_name<T>(), type_name<A>(), C, P, UW, NT, DV, F, U, CH ? ",ch=1" : "", XG ? ",xg=1" : "", MW, XL, ntiles,
              WG, lds, TF, ahead, xcd_remap, self ? " self=1" : "", need);
     g_plan->ws_bytes = need;
     return MAVG_OK;
@@ -614,83 +613,11 @@ int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ah
   p.trace = reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(ws.ptr) + need - trace_bytes);
 #endif
   if (lds > 64 * 1024) {
-    const int s = raise_dyn_lds_limit<&wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH, XG, MW>>(80 * 1024);
+    const int s = raise_dyn_lds_limit<&wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH, XG, MW, XL>>(80 * 1024);
     if (s != MAVG_OK) return s;
   }
-  hipLaunchKernelGGL((wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH, XG, MW>), dim3((unsigned)ntiles), dim3(WG), lds,
+  hipLaunchKernelGGL((wide_ahead_kernel<T, A, C, P, UW, WG, NT, DV, F, U, CH, XG, MW, XL>), dim3((unsigned)ntiles), dim3(WG), lds,
                      st, p);
-  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
-}
-
-// paired look-ahead scan (mavg_pair.hpp): the halo-only channel-per-lane look-ahead with two
-// consecutive tiles per workgroup (tile t + 1 chains tile t's carry); windows short of the L2
-// reach (remap mode 1), 16- or 32-B frames, 16-B-aligned views.  The records and their
-// workspace are the one-tile kernel's (per tile, per virtual slot); the grid is 8 workgroups per
-// pair of run positions.
-template <typename T, typename A, int C, int P, int WG, int NT, int DV, int U>
-int launch_pair_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
-  constexpr int NW = WG / 64;
-  constexpr int EPG = 16 / (int)sizeof(T);
-  constexpr int CL = C * (int)sizeof(T) / 4;
-  constexpr int TF = NW * (64 / CL) * P;
-  static_assert(TF == WG * U, "F = 1 record units");
-  constexpr int TG = TF * C / EPG;
-  using SA = typename ScanAcc<T, A>::type;
-  const long long nframes = sg.nframes;
-  if (ahead_past_l2(k, C, sizeof(T), TF) || (long long)k < TF) return MAVG_ERR_UNSUPPORTED;
-  ahead &= ~7;
-  int spin = kAheadSpin;
-#ifdef MAVG_TEST_HOOKS
-  {
-    const int t = g_test_ahead_slots.load(std::memory_order_relaxed);
-    if (t >= 0) ahead = t & ~7;
-  }
-  {
-    const int t = g_test_ahead_spin.load(std::memory_order_relaxed);
-    if (t >= 0) spin = t;
-  }
-#endif
-  const long long ntiles = (nframes + TF - 1) / TF;
-  const long long nfull = nframes / TF;
-  if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
-  const long long q8 = (ntiles + 7) / 8;               // run positions of the longest run
-  const long long grid = 8 * ((q8 + 1) / 2);           // a workgroup per pair of positions per XCD
-  const size_t need = ahead_granule_bytes<T, A, C, 1, U>(nfull);
-  const size_t lds = (size_t)2 * (TG + 1) * 16 + (size_t)(NW * C + C) * sizeof(A) + (size_t)(2 + 6) * NW * C * sizeof(SA);
-  if (lds > 64 * 1024) return MAVG_ERR_UNSUPPORTED;
-  if (g_plan) {
-    snprintf(g_plan->text, sizeof(g_plan->text),
-             "pair_ahead<%s,acc=%s,C=%d,P=%d,nt=%d,dv=%d,FU=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
-             "ahead=%d remap=1 tiles=%lld ws=%zu",
-             type_name<T>(), type_name<A>(), C, P, NT, DV, U, grid, WG, lds, TF, ahead, ntiles, need);
-    g_plan->ws_bytes = need;
-    return MAVG_OK;
-  }
-  if (ws.ptr == nullptr || ws.bytes < need) return MAVG_ERR_WORKSPACE;
-  if ((reinterpret_cast<uintptr_t>(ws.ptr) & 15u) != 0) return MAVG_ERR_MISALIGNED;
-  if (hipMemsetAsync(ws.ptr, 0, need, st) != hipSuccess) return MAVG_ERR_HIP;
-  AheadParams p{};
-  p.in = sg.in;
-  p.out = sg.out;
-  p.hist = sg.hist;
-  p.nframes = nframes;
-  p.pre = sg.pre;
-  p.eio = 0;
-  p.nfull = nfull;
-  p.k = k;
-  p.o = make_out_params(k);
-  p.halo_units = k;
-  p.xk_off = 0;
-  p.xcd_remap = 1;
-  p.runs_done = 0;
-  p.ahead = ahead;
-  p.head = (int)std::min<long long>((long long)k / TF, nfull);
-  p.spin = spin;
-  p.self = 0;
-  p.gran = static_cast<unsigned long long*>(ws.ptr);
-  p.runs = nullptr;
-  p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
-  hipLaunchKernelGGL((pair_ahead_kernel<T, A, C, P, WG, NT, DV, U>), dim3((unsigned)grid), dim3(WG), lds, st, p);
   return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
@@ -862,15 +789,25 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     // 2048 <= k <= 3584: the halo-only channel-per-lane tile (2048-frame tiles; in-process,
     // profiles/r04_tuning/chan/xg_c4_*, xgr_*: k=2048 0.660 -> 0.712 against the wide tile, 3000
     // 0.541 -> 0.675 against the wide look-ahead; k=4096 ties it, 0.559 vs 0.556)
-    if (k >= 2048 && halo_bytes <= 57344) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true, true>(sg, k, st);
+    // round 6: x of the halo-only forms as 16-B frame loads plus quad transposes (XL, mavg_wide.hpp
+    // xl_load) -- a quarter of the vector-memory transactions of the 4-B column loads.  In-process
+    // (tools/tune/wide_ab.hip "xl", profiles/r06_tuning/xl/): the look-ahead in 2048-frame tiles
+    // (141 VGPRs, D = 384) 0.630-0.639 -> 0.683 at k = 44100, 0.658 -> 0.696 at 20000, 0.6975
+    // against the chan tile's 0.683-0.695 at k = 3000 (no in-place form there).  The in-place chan
+    // tile (k mod 16 = 0) wins up to k = 3072 (2560: 0.716 vs 0.697, 3072: 0.691 vs 0.686), with XL
+    // while four workgroups per CU fit its LDS (k = 2048: 0.728 -> 0.751; k = 2560, three per CU:
+    // 0.716 -> 0.704).  1024-frame look-ahead tiles with XL: 0.636-0.671.
+    const bool ip = k % 16 == 0;  // the staged halo is exactly k frames (chan tile IP)
+    if (k >= 2048 && k <= 3072 && ip) {
+      if (halo_bytes <= 40704) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true, true, 1>(sg, k, st);
+      return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true, true>(sg, k, st);
+    }
     if (halo_bytes <= 4096) return launch_wide_tile<T, A, C, 8, 2, kWG, kNtS>(sg, k, st);
     if (halo_bytes <= 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
-    // past the halo-only tile: the halo-only channel-per-lane look-ahead (round 5, in-process,
+    // past the chan tile: the halo-only channel-per-lane look-ahead (round 5, in-process,
     // profiles/r05_tuning/wide/pa0_c4_k44100.log: k=44100 0.540 -> 0.593 against the chunk
-    // look-ahead), in 1024-frame tiles (16 frames per lane, 92 VGPRs, D = 768) rather than 2048
-    // (142 VGPRs): 0.612 -> 0.622 and 0.612 -> 0.617 on two boxes (after_butterfly/ab_f32_c4_k44100,
-    // ab_f32_c4_k44100_mw4)
-    return launch_wide_ahead<T, A, C, 16, 1, kWG, kNtA, 0, 1, 4, true, true>(sg, k, st, ws, 768);
+    // look-ahead), with XL in 2048-frame tiles (above)
+    return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 8, true, true, 0, 1>(sg, k, st, ws, 384);
   } else if constexpr (sizeof(T) == 4 && C == 8) {
     // one channel per lane (chan_tile_kernel, 32 frames each): one scan per
     // tile row for all 8 channels instead of 8 per chunk (in-process A/B,
@@ -916,8 +853,11 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
       // 0.589 -> 0.652 against the wide tile)
       if (halo_bytes <= 49152) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
     }
-    // past it the halo-only channel-per-lane look-ahead (int32 sums: k <= 65535)
-    if constexpr (sizeof(A) == 4) return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 8, true, true>(sg, k, st, ws, 384);
+    // past it the halo-only channel-per-lane look-ahead (int32 sums: k <= 65535), with x as 16-B
+    // frame loads (XL, round 6; in-process, profiles/r06_tuning/xl/: k = 44100 0.592-0.600 ->
+    // 0.609, 20000 0.600-0.612 -> 0.624, 3072 0.611 -> 0.625)
+    if constexpr (sizeof(A) == 4)
+      return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 8, true, true, 0, 1>(sg, k, st, ws, 384);
     return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
   }
   (void)halo_bytes;

@@ -409,16 +409,51 @@ template <> struct ChanElem<int16_t> {
   }
 };
 
+// XL (round 6, the halo-only forms with 16-B frames: fp32 4 channels, int16 8 channels): a lane's
+// column of P frames j0 .. j0 + P - 1 loaded as whole 16-B frames -- lane cl of the block's quad
+// takes frames j0 + 4m + cl, 64 contiguous bytes per quad and wave instruction -- and turned into
+// the column by quad transposes (quad_transpose4) once the first barrier has passed, so the loads
+// stay in flight behind everything issued after them.  The 4-B column loads fetched 16 separate
+// 16-B pieces per wave instruction, four times the vector-memory transactions for the same bytes.
+// Every tile loads this way: its frames are >= 0, so only the end needs care -- frames past it
+// read the last frame (outputs there are not stored).  No branch between two load forms: such a
+// merge made the compiler wait for these loads before issuing the stage.
+template <int P>
+__device__ __forceinline__ void xl_load(const void* in, long long f0, int cl, long long nframes, uint32_t (&xr)[P]) {
+  static_assert(P % 4 == 0, "whole quads of frames");
+  const u32x4* in4 = static_cast<const u32x4*>(in);
+  const long long last = nframes - 1;
+#pragma unroll
+  for (int m = 0; m < P / 4; ++m) {
+    const long long f = f0 + 4 * m + cl;
+    const u32x4 v = in4[f < last ? f : last];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xr[4 * m + q] = v[q];
+  }
+}
+template <int P>
+__device__ __forceinline__ void xl_transpose(uint32_t (&xr)[P], int cl) {
+#pragma unroll
+  for (int m = 0; m < P / 4; ++m) {
+    uint32_t q4[4] = {xr[4 * m], xr[4 * m + 1], xr[4 * m + 2], xr[4 * m + 3]};
+    quad_transpose4(q4, cl);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) xr[4 * m + f] = q4[f];
+  }
+}
+
 // IP (XG only, the launcher's choice when the staged halo is exactly k frames): each output is
 // written in pass 2 over the x[n-k] it last read -- the same lane and address, as in the wide
 // look-ahead -- so no barrier before the output stage and no Q output registers
-template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false, bool IP = false>
+template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false, bool IP = false,
+          int XL = 0>
 __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   static_assert(!IP || XG, "in-place outputs need the halo-only stage");
   using CE = ChanElem<T>;
   constexpr int E = CE::E;      // samples (channels) per dword
   constexpr int CL = C / E;     // dword columns per frame
   static_assert(C % E == 0 && (CL == 4 || CL == 8), "frames of 16 or 32 bytes");
+  static_assert(XL == 0 || (XG && CL == 4), "16-B frame loads: the halo-only form with 16-B frames");
   constexpr int NW = WG / 64;
   constexpr int NB = 64 / CL;   // frame blocks per wave
   constexpr int GPF = CL / 4;   // 16-B granules per frame
@@ -462,7 +497,9 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   const int b = lane / CL;
   const int jl = w * WF + b * Q;  // tile frame of the lane's first frame
   uint32_t xr[XG ? Q : 1];
-  if constexpr (XG) {  // the lane's x, issued before the stage
+  if constexpr (XG && XL == 1) {
+    xl_load<Q>(in, t0 + jl, c, nframes, xr);
+  } else if constexpr (XG) {  // the lane's x, issued before the stage
     if (tile_full) {
       const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
 #pragma unroll
@@ -553,6 +590,7 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   }
 
   // ---- pass 1: the lane's channels over its Q frames; the scan across its NB lanes ----
+  if constexpr (XL == 1) xl_transpose<Q>(xr, c);
   const int f0 = Hf + jl;  // stage frame of the lane's first frame
   auto xv = [&](int i) -> uint32_t {
     if constexpr (XG) return xr[i];
@@ -713,8 +751,11 @@ namespace mavg {
 // the halo-only form held 142-228 VGPRs (forcing 128 for fp32 C = 4 spilled,
 // 0.612 -> 0.50 of peak); the register work that followed (126 VGPRs at C = 8,
 // 92 at C = 4) reaches the LDS-sized 4 workgroups per CU without it.
+// XL (round 6, XG with 16-B frames): x as 16-B frame loads plus quad transposes (xl_load,
+// chan_tile_kernel), transposed after the first barrier so the loads stay in flight behind the
+// stage and phase A.
 template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false,
-          bool XG = false, int MW = 0>
+          bool XG = false, int MW = 0, int XL = 0>
 __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadParams p) {
   constexpr int NW = WG / 64;
   constexpr int EPG = 16 / (int)sizeof(T);
@@ -729,6 +770,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   constexpr int E = CEl::E;
   constexpr int CL = C / E > 0 ? C / E : 1;  // CH: dword columns per frame (a lane owns one)
   static_assert(!CH || (UW == 1 && C % E == 0 && (CL == 4 || CL == 8)), "channel-per-lane form: 16- or 32-B frames");
+  static_assert(XL == 0 || (XG && CL == 4 && P % 4 == 0), "16-B frame loads: the halo-only form with 16-B frames");
   constexpr int QM = G == 4 ? 3 : 7;
   constexpr int NB = 64 / CL;              // CH: frame blocks per wave
   constexpr int WF = NB * P;               // CH: frames per wave
@@ -801,7 +843,9 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   const int j0 = w * WF + (lane / CL) * P;
   uint32_t xr[XG ? P : 1];
   auto load_x = [&]() {
-    if (tile_full) {
+    if constexpr (XL == 1) {
+      xl_load<P>(in, t0 + j0, cl, nframes, xr);  // every tile (transposed after the first barrier)
+    } else if (tile_full) {
       const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
 #pragma unroll
       for (int i = 0; i < P; ++i) xr[i] = in32[(t0 + j0 + i) * CL + cl];
@@ -1064,6 +1108,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
       if (lane >= 64 - CL) tot[w * C + cl * E + e] = cincl[e];
     }
   };
+  if constexpr (XL == 1) xl_transpose<P>(xr, cl);
   if constexpr (CH) ch_pass1();
   SA lx[UW][C];
 #pragma unroll

@@ -187,14 +187,21 @@ def test_plan_describes_launch_without_gpu():
     assert ",xg=1>" in dsp.plan(1 << 30, 1024, channels=8) and ",xg=1>" not in dsp.plan(1 << 30, 511, channels=8)
     # past the halo-only tile (8 channels k > 1536, 4 channels k > 3584): the halo-only channel-per-lane
     # look-ahead (x from global memory, only the shifted tile in LDS)
-    for C, k in ((8, 1537), (8, 44100), (4, 3585), (4, 44100)):
+    # (round 6: with 16-B frames x comes as whole-frame loads turned into columns, xl=1)
+    for C, k in ((8, 1537), (8, 44100), (4, 2561), (4, 3000), (4, 3088), (4, 44100)):
         p = dsp.plan(1 << 30, k, channels=C)
-        assert p.startswith(f"wide_ahead<f32,acc=f64,C={C},P={32 if C == 8 else 16}") and ",ch=1,xg=1," in p, p
-    assert ",xg=1>" in dsp.plan(1 << 30, 1536, channels=8) and ",xg=1>" in dsp.plan(1 << 30, 3000, channels=4)
+        assert p.startswith(f"wide_ahead<f32,acc=f64,C={C},P=32") and ",ch=1,xg=1," in p, p
+        assert (",xl=1>" in p) == (C == 4), p
+    assert ",xg=1>" in dsp.plan(1 << 30, 1536, channels=8)
+    for k in (2048, 2544, 2560, 3072):  # the in-place chan tile (staged halo of exactly k frames),
+        p = dsp.plan(1 << 30, k, channels=4)  # with XL while 4 workgroups per CU fit its LDS (160 KiB)
+        want = ",xg=1,ip=1,xl=1>" if k <= 2544 else ",xg=1,ip=1>"
+        assert p.startswith("chan_tile<f32,acc=f64,C=4,Q=32") and want in p, p
     # int16 8 channels: a dword column (two channels) per lane from a window of one tile on
     i16c8 = lambda k: dsp.plan(1 << 30, k, channels=8, dtype=dsp.I16)
     assert i16c8(1024).startswith("wide_tile<i16") and i16c8(2048).startswith("chan_tile<i16,acc=i32,C=8,Q=32")
     assert i16c8(44100).startswith("wide_ahead<i16,acc=i32,C=8,P=32") and ",ch=1,xg=1," in i16c8(44100)
+    assert ",xl=1>" in i16c8(44100) and ",xl=1>" in i16c8(3073)
     # aggregate-first look-ahead records in 32-KiB tiles (round 6): int16 mono / stereo past a
     # 16-KiB halo, int16 4 channels past 64 KiB, fp32 stereo past the wide tile's 32 KiB, short of
     # the L2 reach (int16 mono: k <= 131072); fp32 mono and 8 channels keep their kernels
@@ -210,8 +217,8 @@ def test_plan_describes_launch_without_gpu():
     assert far(i16(4_000_000, 2)) and " self=1 " in i16(4_000_000, 2) and " ahead=960 " in i16(4_000_000, 2)
     assert far(i16(1_500_000, 1)) and " self=1 " in i16(1_500_000, 1)
     assert far(i16(4_000_000, 1)) and " self=1 " not in i16(4_000_000, 1)
-    for k in (600_000, 1_000_000, 4_000_000, 8_000_000):
-        assert far(dsp.plan(1 << 30, k)) and " self=1 " in dsp.plan(1 << 30, k), k
+    for k in (600_000, 1_000_000, 4_000_000, 8_000_000):  # fp32 mono: phase A (bench.py's timing)
+        assert far(dsp.plan(1 << 30, k)) and " self=1 " not in dsp.plan(1 << 30, k), k
     assert "runs=1" in dsp.plan(1 << 30, 9_000_000)  # past 1024 tiles: the run-total kernel
     assert i16(8192, 4).startswith("wide_ahead<") and agg(i16(8193, 4)) and agg(i16(100_000, 4))
     assert dsp.plan(1 << 30, 4096, channels=2).startswith("wide_tile<") and agg(dsp.plan(1 << 30, 4097, channels=2))

@@ -63,11 +63,11 @@ def plan_key(plan):
         args = (T, acc, kv["C"], kv["P"], kv["U"], wg, kv["nt"], kv.get("dv", "0"))
     elif fam == "chan_tile":
         args = (T, acc, kv["C"], kv["Q"], wg, kv["nt"], kv.get("dv", "0"), "true" if kv.get("xg", "0") == "1" else "false",
-                "true" if kv.get("ip", "0") == "1" else "false")
+                "true" if kv.get("ip", "0") == "1" else "false", kv.get("xl", "0"))
     elif fam == "wide_ahead":
         args = (T, acc, kv["C"], kv["P"], kv["U"], wg, kv["nt"], kv.get("dv", "0"), kv["F"], kv["FU"],
                 "true" if kv.get("ch", "0") == "1" else "false", "true" if kv.get("xg", "0") == "1" else "false",
-                kv.get("mw", "0"))
+                kv.get("mw", "0"), kv.get("xl", "0"))
     else:
         args = (T, acc)
     return FAMILY[fam], args

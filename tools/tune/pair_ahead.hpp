@@ -1,9 +1,11 @@
-// mavg_pair.hpp -- the paired look-ahead scan (pair_ahead_kernel): the halo-only channel-per-lane
-// look-ahead of mavg_wide.hpp (wide_ahead_kernel, CH + XG) with TWO consecutive tiles per
-// workgroup, whose bytes are all in flight at once.
+// pair_ahead.hpp -- round-6 experiment, tuner only (tools/tune/wide_ab.hip "pair"): the paired
+// look-ahead scan (pair_ahead_kernel), the halo-only channel-per-lane look-ahead of
+// mavg_wide.hpp (wide_ahead_kernel, CH + XG) with TWO consecutive tiles per workgroup, whose
+// bytes are all in flight at once.  Not in the library: it measured a tie at best against the
+// one-tile kernel in 2048-frame tiles (profiles/r06_tuning/pair/, xl/).
 #pragma once
 
-#include "mavg_wide.hpp"
+#include "../../digital_signal_processsing_amd/csrc/mavg_launch.hpp"
 
 namespace mavg {
 
@@ -31,7 +33,8 @@ namespace mavg {
 // Windows short of the L2 reach only (remap mode 1: consecutive slots of a run hold consecutive
 // tiles).
 // ----------------------------------------------------------------------------
-template <typename T, typename A, int C, int P, int WG, int NT, int DV, int U>
+// XL: x as 16-B frame loads plus quad transposes (mavg_wide.hpp xl_load; 16-B frames)
+template <typename T, typename A, int C, int P, int WG, int NT, int DV, int U, int XL = 0>
 __global__ __launch_bounds__(WG) void pair_ahead_kernel(AheadParams p) {
   constexpr int F = 1;
   constexpr int NW = WG / 64;
@@ -40,6 +43,7 @@ __global__ __launch_bounds__(WG) void pair_ahead_kernel(AheadParams p) {
   constexpr int E = CEl::E;
   constexpr int CL = C / E;  // dword columns per frame (a lane owns one)
   static_assert(C % E == 0 && (CL == 4 || CL == 8), "16- or 32-B frames");
+  static_assert(XL == 0 || CL == 4, "16-B frame loads: 16-B frames");
   constexpr int NB = 64 / CL;   // frame blocks per wave
   constexpr int WF = NB * P;    // frames per wave
   constexpr int TF = NW * WF;   // frames per tile
@@ -98,7 +102,9 @@ __global__ __launch_bounds__(WG) void pair_ahead_kernel(AheadParams p) {
   const int j0 = w * WF + (lane / CL) * P;
   uint32_t xr0[P], xr1[P];
   auto load_x = [&](long long t0, bool full, uint32_t (&xr)[P]) {
-    if (full) {
+    if constexpr (XL == 1) {
+      xl_load<P>(in, t0 + j0, cl, nframes, xr);
+    } else if (full) {
       const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
 #pragma unroll
       for (int i = 0; i < P; ++i) xr[i] = in32[(t0 + j0 + i) * CL + cl];
@@ -242,7 +248,7 @@ __global__ __launch_bounds__(WG) void pair_ahead_kernel(AheadParams p) {
   // stage frame f): element (j0 + i, cl) at float index tb[i mod NBX] + (i / NBX) NBX 4 GPF
   constexpr int GPFc = CL >= 4 ? CL / 4 : 1;
   constexpr int NBX = NB < P ? NB : P;
-  static_assert(NBX * (P / NBX) == P, "whole address-table rounds");
+  static_assert(NBX * (P / NBX) == P && P >= NB, "whole address-table rounds; chan_slot keys inside a lane's frames");
   constexpr int kFS = 4 * GPFc;  // floats per frame of the stage
   auto ch_table = [&](int lb, int bq, int (&tb)[NBX]) {
 #pragma unroll
@@ -288,6 +294,10 @@ __global__ __launch_bounds__(WG) void pair_ahead_kernel(AheadParams p) {
       if (lane >= 64 - CL) totw[w * C + cl * E + e] = cincl[e];
     }
   };
+  if constexpr (XL == 1) {
+    xl_transpose<P>(xr0, cl);
+    if (has2) xl_transpose<P>(xr1, cl);
+  }
   if (pcount > wq * WF) pass1(xr0, sst[0], crun0, cincl0, tot, std::true_type{});
   else pass1(xr0, sst[0], crun0, cincl0, tot, std::false_type{});
   if (has2) pass1(xr1, sst[1], crun1, cincl1, tot + NW * C, std::false_type{});
@@ -461,6 +471,78 @@ __global__ __launch_bounds__(WG) void pair_ahead_kernel(AheadParams p) {
     }
     pass2(t01, full1, xr1, sst[1], base, run);
   }
+}
+
+// paired look-ahead scan (pair_ahead_kernel above): the halo-only channel-per-lane look-ahead with two
+// consecutive tiles per workgroup (tile t + 1 chains tile t's carry); windows short of the L2
+// reach (remap mode 1), 16- or 32-B frames, 16-B-aligned views.  The records and their
+// workspace are the one-tile kernel's (per tile, per virtual slot); the grid is 8 workgroups per
+// pair of run positions.
+template <typename T, typename A, int C, int P, int WG, int NT, int DV, int U, int XL = 0>
+int launch_pair_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead) {
+  constexpr int NW = WG / 64;
+  constexpr int EPG = 16 / (int)sizeof(T);
+  constexpr int CL = C * (int)sizeof(T) / 4;
+  constexpr int TF = NW * (64 / CL) * P;
+  static_assert(TF == WG * U, "F = 1 record units");
+  constexpr int TG = TF * C / EPG;
+  using SA = typename ScanAcc<T, A>::type;
+  const long long nframes = sg.nframes;
+  if (ahead_past_l2(k, C, sizeof(T), TF) || (long long)k < TF) return MAVG_ERR_UNSUPPORTED;
+  ahead &= ~7;
+  int spin = kAheadSpin;
+#ifdef MAVG_TEST_HOOKS
+  {
+    const int t = g_test_ahead_slots.load(std::memory_order_relaxed);
+    if (t >= 0) ahead = t & ~7;
+  }
+  {
+    const int t = g_test_ahead_spin.load(std::memory_order_relaxed);
+    if (t >= 0) spin = t;
+  }
+#endif
+  const long long ntiles = (nframes + TF - 1) / TF;
+  const long long nfull = nframes / TF;
+  if (ntiles > 0x7fffffffLL) return MAVG_ERR_UNSUPPORTED;
+  const long long q8 = (ntiles + 7) / 8;               // run positions of the longest run
+  const long long grid = 8 * ((q8 + 1) / 2);           // a workgroup per pair of positions per XCD
+  const size_t need = ahead_granule_bytes<T, A, C, 1, U>(nfull);
+  const size_t lds = (size_t)2 * (TG + 1) * 16 + (size_t)(NW * C + C) * sizeof(A) + (size_t)(2 + 6) * NW * C * sizeof(SA);
+  if (lds > 64 * 1024) return MAVG_ERR_UNSUPPORTED;
+  if (g_plan) {
+    snprintf(g_plan->text, sizeof(g_plan->text),
+             "pair_ahead<%s,acc=%s,C=%d,P=%d,nt=%d,dv=%d,FU=%d,xl=%d> grid=%lld block=%d lds=%zu tile_frames=%d "
+             "ahead=%d remap=1 tiles=%lld ws=%zu",
+             type_name<T>(), type_name<A>(), C, P, NT, DV, U, XL, grid, WG, lds, TF, ahead, ntiles, need);
+    g_plan->ws_bytes = need;
+    return MAVG_OK;
+  }
+  if (ws.ptr == nullptr || ws.bytes < need) return MAVG_ERR_WORKSPACE;
+  if ((reinterpret_cast<uintptr_t>(ws.ptr) & 15u) != 0) return MAVG_ERR_MISALIGNED;
+  if (hipMemsetAsync(ws.ptr, 0, need, st) != hipSuccess) return MAVG_ERR_HIP;
+  AheadParams p{};
+  p.in = sg.in;
+  p.out = sg.out;
+  p.hist = sg.hist;
+  p.nframes = nframes;
+  p.pre = sg.pre;
+  p.eio = 0;
+  p.nfull = nfull;
+  p.k = k;
+  p.o = make_out_params(k);
+  p.halo_units = k;
+  p.xk_off = 0;
+  p.xcd_remap = 1;
+  p.runs_done = 0;
+  p.ahead = ahead;
+  p.head = (int)std::min<long long>((long long)k / TF, nfull);
+  p.spin = spin;
+  p.self = 0;
+  p.gran = static_cast<unsigned long long*>(ws.ptr);
+  p.runs = nullptr;
+  p.stats = static_cast<unsigned char*>(ws.ptr) + need - 16;
+  hipLaunchKernelGGL((pair_ahead_kernel<T, A, C, P, WG, NT, DV, U, XL>), dim3((unsigned)grid), dim3(WG), lds, st, p);
+  return hipGetLastError() == hipSuccess ? MAVG_OK : MAVG_ERR_HIP;
 }
 
 }  // namespace mavg

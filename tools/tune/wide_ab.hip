@@ -5,7 +5,7 @@
 // checked against the library's (|dy| <= 1e-6 |y|, fp64 sums in another order).
 //
 // build: make -C tools/tune wide_ab
-// run:   tools/tune/wide_ab <log2n> <k> <C> [rounds] [dist] [f32|i16] [hs|self|selfhs|pair]
+// run:   tools/tune/wide_ab <log2n> <k> <C> [rounds] [dist] [f32|i16] [hs|self|selfhs|pair|xl]
 // A copy of this file built against another tree's headers (round 5's wide_ab_prev / _cand /
 // _r04) compares that tree's kernels with this library's: the library is linked -Bsymbolic, so
 // its launches keep its own kernel code even where the template instances share a name.
@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../digital_signal_processsing_amd/csrc/mavg_launch.hpp"
+#include "pair_ahead.hpp"
 
 using namespace mavg;
 
@@ -47,11 +48,11 @@ void add1(std::vector<Var>& vs, const Sig& sg, int k) {
 }
 
 template <typename T, typename A, int C, int Q, int WG, bool XG = false, int NT = kNtSplit | kNtHalo | kNtStore,
-          bool IPOK = false>
+          bool IPOK = false, int XL = 0>
 void addC(std::vector<Var>& vs, const Sig& sg, int k) {
   char name[64];
-  snprintf(name, sizeof name, "chan Q%d %d nt%d xg%d%s", Q, WG, NT, (int)XG, XG && IPOK ? " ip" : "");
-  vs.push_back({name, [=](hipStream_t s) { return launch_chan_tile<T, A, C, Q, WG, NT, 0, XG, IPOK>(sg, k, s); }, {}});
+  snprintf(name, sizeof name, "chan Q%d %d nt%d xg%d%s%s", Q, WG, NT, (int)XG, XG && IPOK ? " ip" : "", XL ? " xl1" : "");
+  vs.push_back({name, [=](hipStream_t s) { return launch_chan_tile<T, A, C, Q, WG, NT, 0, XG, IPOK, XL>(sg, k, s); }, {}});
 }
 
 // the round-3 unit kernels for the same C (tile_scan / ahead_scan, 32-B or 64-B units)
@@ -89,15 +90,47 @@ void addU(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D, size_
 }
 
 // the wide look-ahead scan with the channel-per-lane in-tile scan (CH)
-template <typename T, typename A, int C, int Q, int WG, int F, int U, bool XG = false, int MW = 0>
+template <typename T, typename A, int C, int Q, int WG, int F, int U, bool XG = false, int MW = 0, int XL = 0>
 void addAC(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D, bool self = false) {
   constexpr int kNtA = kNtStore | kNtHalo;
   char name[80];
-  snprintf(name, sizeof name, "wahead chan Q%d %d F%d U%d D%d xg%d mw%d%s", Q, WG, F, U, D, (int)XG, MW,
-           self ? " self" : "");
+  snprintf(name, sizeof name, "wahead chan Q%d %d F%d U%d D%d xg%d mw%d%s%s", Q, WG, F, U, D, (int)XG, MW,
+           self ? " self" : "", XL ? " xl1" : "");
   vs.push_back({name, [=](hipStream_t s) {
-                  return launch_wide_ahead<T, A, C, Q, 1, WG, kNtA, 0, F, U, true, XG, MW>(sg, k, s, ws, D, self);
+                  return launch_wide_ahead<T, A, C, Q, 1, WG, kNtA, 0, F, U, true, XG, MW, XL>(sg, k, s, ws, D, self);
                 }, {}});
+}
+// round 6: x of the halo-only channel-per-lane look-ahead as 16-B frame loads + quad transposes (XL)
+// against the 4-B column loads, 16-B frames (fp32 4 channels, int16 8 channels)
+template <typename T, typename A, int C>
+void add_xl(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
+  constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
+  if (k <= 4096) {  // the halo-only channel tile's range (fp32 C = 4: k <= 3584, int16 C = 8: k <= 3072)
+    if constexpr (sizeof(T) == 4 && C == 4) {
+      addC<T, A, C, 32, 256, true, kNtS, true>(vs, sg, k);
+      addC<T, A, C, 32, 256, true, kNtS, true, 1>(vs, sg, k);
+      addC<T, A, C, 16, 256, true, kNtS, true, 1>(vs, sg, k);
+    } else if constexpr (sizeof(T) == 2 && C == 8) {
+      addC<T, A, C, 32, 256, true>(vs, sg, k);
+      addC<T, A, C, 32, 256, true, kNtS, false, 1>(vs, sg, k);
+      addC<T, A, C, 16, 256, true, kNtS, false, 1>(vs, sg, k);
+    }
+  }
+  if constexpr (sizeof(T) == 4 && C == 4) {
+    addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 768);
+    addAC<T, A, C, 16, 256, 1, 4, true, 0, 1>(vs, sg, k, ws, 768);
+    for (int D : {256, 320, 384, 448}) addAC<T, A, C, 32, 256, 1, 8, true, 0, 1>(vs, sg, k, ws, D);
+    addAC<T, A, C, 32, 256, 1, 8, true, 4, 1>(vs, sg, k, ws, 384);
+    addAC<T, A, C, 32, 128, 1, 8, true, 0, 1>(vs, sg, k, ws, 768);
+    addP<T, A, C, 16, 256, 4, 1>(vs, sg, k, ws, 768);
+    addP<T, A, C, 16, 256, 4, 1>(vs, sg, k, ws, 1024);
+  } else if constexpr (sizeof(T) == 2 && C == 8) {
+    addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 384);
+    for (int D : {384, 512, 640}) addAC<T, A, C, 32, 256, 1, 8, true, 0, 1>(vs, sg, k, ws, D);
+    addAC<T, A, C, 32, 512, 1, 8, true, 0, 1>(vs, sg, k, ws, 384, true);
+    addAC<T, A, C, 32, 512, 1, 8, true, 0, 1>(vs, sg, k, ws, 384);
+    addP<T, A, C, 16, 256, 4, 1>(vs, sg, k, ws, 768);
+  }
 }
 
 // the Hillis-Steele look-ahead (mono / stereo) at several look-ahead distances; per-wave records
@@ -168,19 +201,18 @@ void add_self(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, bool hs)
 
 // round 6: the paired look-ahead (mavg_pair.hpp, two consecutive tiles per workgroup) against the
 // one-tile halo-only channel-per-lane look-ahead at the same tile shape
-template <typename T, typename A, int C, int Q, int WG, int U>
+template <typename T, typename A, int C, int Q, int WG, int U, int XL = 0>
 void addP(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D) {
   constexpr int kNtA = kNtStore | kNtHalo;
   char name[80];
-  snprintf(name, sizeof name, "pair chan Q%d %d U%d D%d", Q, WG, U, D);
-  vs.push_back({name, [=](hipStream_t s) { return launch_pair_ahead<T, A, C, Q, WG, kNtA, 0, U>(sg, k, s, ws, D); }, {}});
+  snprintf(name, sizeof name, "pair chan Q%d %d U%d D%d%s", Q, WG, U, D, XL ? " xl1" : "");
+  vs.push_back({name, [=](hipStream_t s) { return launch_pair_ahead<T, A, C, Q, WG, kNtA, 0, U, XL>(sg, k, s, ws, D); }, {}});
 }
 template <typename T, typename A, int C>
 void add_pair(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   if constexpr (sizeof(T) == 4 && C == 4) {
     addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 768);
     for (int D : {384, 768, 1024, 1536}) addP<T, A, C, 16, 256, 4>(vs, sg, k, ws, D);
-    addP<T, A, C, 8, 256, 2>(vs, sg, k, ws, 1536);
   } else if constexpr (sizeof(T) == 4 && C == 8) {
     addAC<T, A, C, 32, 256, 1, 4, true>(vs, sg, k, ws, 384);
     addAC<T, A, C, 16, 256, 1, 2, true>(vs, sg, k, ws, 768);
@@ -366,6 +398,7 @@ int main(int argc, char** argv) {
   const bool selfab = argc > 7 && (std::string(argv[7]) == "self" || std::string(argv[7]) == "selfhs");
   const bool selfhs = argc > 7 && std::string(argv[7]) == "selfhs";
   const bool pairab = argc > 7 && std::string(argv[7]) == "pair";  // the paired look-ahead (add_pair)
+  const bool xlab = argc > 7 && std::string(argv[7]) == "xl";  // 16-B frame loads (add_xl)
   const int algo = hs || selfhs ? MAVG_ALGO_HILLIS : MAVG_ALGO_BLELLOCH;
   const int dt = i16 ? MAVG_I16 : MAVG_F32;
   const int eb = i16 ? 2 : 4;
@@ -393,7 +426,13 @@ int main(int argc, char** argv) {
                 }, {}});
   vs.push_back({"copy", [=](hipStream_t s) { return mavg_stream_copy(x, y, n * eb, s); }, {}});
   const Workspace w2{ws, ws2};
-  if (pairab) {
+  if (xlab) {
+    switch (C * (i16 ? -1 : 1)) {
+      case 4: add_xl<float, double, 4>(vs, sg, k, w2); break;
+      case -8: add_xl<int16_t, int32_t, 8>(vs, sg, k, w2); break;
+      default: fprintf(stderr, "xl: f32 C=4, i16 C=8\n"); return 1;
+    }
+  } else if (pairab) {
     switch (C * (i16 ? -1 : 1)) {
       case 4: add_pair<float, double, 4>(vs, sg, k, w2); break;
       case 8: add_pair<float, double, 8>(vs, sg, k, w2); break;
