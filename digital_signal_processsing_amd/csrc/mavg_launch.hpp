@@ -196,7 +196,7 @@ int launch_wide_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRema
 // in-place output form (chan_tile_kernel IP).  In-process (profiles/r05_tuning/wide/ip_*): fp32
 // C = 4 k=2048 0.737 -> 0.756; fp32 C = 8 k=1024 0.750 -> 0.746 and int16 C = 8 k=2048 0.649 ->
 // 0.485 (170 VGPRs, 2 workgroups per CU), so only fp32 C = 4 asks for it
-// XL: x as 16-B frame loads plus quad transposes (mavg_wide.hpp xl_load; XG with 16-B frames)
+// XL: x as 16-B frame-piece loads plus quad transposes (mavg_wide.hpp xl_load; XG only)
 template <typename T, typename A, int C, int Q, int WG, int NT, int DV = 0, bool XG = false, bool IPOK = false,
           int XL = 0>
 int launch_chan_tile(const Sig& sg, int k, hipStream_t st, int xcd_remap = kRemapGroup) {

@@ -409,24 +409,28 @@ template <> struct ChanElem<int16_t> {
   }
 };
 
-// XL (round 6, the halo-only forms with 16-B frames: fp32 4 channels, int16 8 channels): a lane's
-// column of P frames j0 .. j0 + P - 1 loaded as whole 16-B frames -- lane cl of the block's quad
-// takes frames j0 + 4m + cl, 64 contiguous bytes per quad and wave instruction -- and turned into
-// the column by quad transposes (quad_transpose4) once the first barrier has passed, so the loads
-// stay in flight behind everything issued after them.  The 4-B column loads fetched 16 separate
-// 16-B pieces per wave instruction, four times the vector-memory transactions for the same bytes.
-// Every tile loads this way: its frames are >= 0, so only the end needs care -- frames past it
-// read the last frame (outputs there are not stored).  No branch between two load forms: such a
-// merge made the compiler wait for these loads before issuing the stage.
-template <int P>
+// XL (round 6, the halo-only forms): a lane's column of P frames j0 .. j0 + P - 1 loaded as
+// 16-B pieces of whole frames and turned into the column by quad transposes (quad_transpose4),
+// once the first barrier has passed so the loads stay in flight behind everything issued after
+// them.  Lane l = cl of its block's CL lanes loads, for each group of 4 frames j0 + 4m .. + 3,
+// the 16 bytes at frame j0 + 4m + (cl mod 4), byte 16 (cl / 4) -- the block's CL lanes read the
+// group's 4 CL dwords, 64 (CL = 4) or 128 (CL = 8) contiguous bytes per wave instruction.  In
+// bit terms the lane index is (byte half, frame bits 1..0) and the 4 registers are dword bits
+// 1..0; the transpose swaps lane bits 1..0 with register bits 1..0, leaving dword cl of the 4
+// frames in the lane's 4 registers.  The 4-B column loads fetched 16 (CL = 4) or 8 (CL = 8)
+// separate 16-B / 32-B pieces per wave instruction: four times the vector-memory transactions
+// for the same bytes.  Every tile loads this way: its frames are >= 0, so only the end needs
+// care -- frames past it read the last frame (outputs there are not stored).  No branch between
+// two load forms: such a merge made the compiler wait for these loads before issuing the stage.
+template <int P, int CL>
 __device__ __forceinline__ void xl_load(const void* in, long long f0, int cl, long long nframes, uint32_t (&xr)[P]) {
-  static_assert(P % 4 == 0, "whole quads of frames");
-  const u32x4* in4 = static_cast<const u32x4*>(in);
+  static_assert(P % 4 == 0 && (CL == 4 || CL == 8), "whole quads of frames, 16- or 32-B frames");
+  const uint32_t* in32 = static_cast<const uint32_t*>(in);
   const long long last = nframes - 1;
 #pragma unroll
   for (int m = 0; m < P / 4; ++m) {
-    const long long f = f0 + 4 * m + cl;
-    const u32x4 v = in4[f < last ? f : last];
+    const long long f = f0 + 4 * m + (cl & 3);
+    const u32x4 v = *reinterpret_cast<const u32x4*>(in32 + (f < last ? f : last) * CL + 4 * (cl >> 2));
 #pragma unroll
     for (int q = 0; q < 4; ++q) xr[4 * m + q] = v[q];
   }
@@ -436,7 +440,7 @@ __device__ __forceinline__ void xl_transpose(uint32_t (&xr)[P], int cl) {
 #pragma unroll
   for (int m = 0; m < P / 4; ++m) {
     uint32_t q4[4] = {xr[4 * m], xr[4 * m + 1], xr[4 * m + 2], xr[4 * m + 3]};
-    quad_transpose4(q4, cl);
+    quad_transpose4(q4, cl & 3);
 #pragma unroll
     for (int f = 0; f < 4; ++f) xr[4 * m + f] = q4[f];
   }
@@ -453,7 +457,7 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   constexpr int E = CE::E;      // samples (channels) per dword
   constexpr int CL = C / E;     // dword columns per frame
   static_assert(C % E == 0 && (CL == 4 || CL == 8), "frames of 16 or 32 bytes");
-  static_assert(XL == 0 || (XG && CL == 4), "16-B frame loads: the halo-only form with 16-B frames");
+  static_assert(XL == 0 || XG, "16-B frame-piece loads: the halo-only form");
   constexpr int NW = WG / 64;
   constexpr int NB = 64 / CL;   // frame blocks per wave
   constexpr int GPF = CL / 4;   // 16-B granules per frame
@@ -498,7 +502,7 @@ __global__ __launch_bounds__(WG) void chan_tile_kernel(WideParams p) {
   const int jl = w * WF + b * Q;  // tile frame of the lane's first frame
   uint32_t xr[XG ? Q : 1];
   if constexpr (XG && XL == 1) {
-    xl_load<Q>(in, t0 + jl, c, nframes, xr);
+    xl_load<Q, CL>(in, t0 + jl, c, nframes, xr);
   } else if constexpr (XG) {  // the lane's x, issued before the stage
     if (tile_full) {
       const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
@@ -751,9 +755,8 @@ namespace mavg {
 // the halo-only form held 142-228 VGPRs (forcing 128 for fp32 C = 4 spilled,
 // 0.612 -> 0.50 of peak); the register work that followed (126 VGPRs at C = 8,
 // 92 at C = 4) reaches the LDS-sized 4 workgroups per CU without it.
-// XL (round 6, XG with 16-B frames): x as 16-B frame loads plus quad transposes (xl_load,
-// chan_tile_kernel), transposed after the first barrier so the loads stay in flight behind the
-// stage and phase A.
+// XL (round 6, XG): x as 16-B frame-piece loads plus quad transposes (xl_load), transposed after
+// the first barrier so the loads stay in flight behind the stage and phase A.
 template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false,
           bool XG = false, int MW = 0, int XL = 0>
 __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadParams p) {
@@ -770,7 +773,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   constexpr int E = CEl::E;
   constexpr int CL = C / E > 0 ? C / E : 1;  // CH: dword columns per frame (a lane owns one)
   static_assert(!CH || (UW == 1 && C % E == 0 && (CL == 4 || CL == 8)), "channel-per-lane form: 16- or 32-B frames");
-  static_assert(XL == 0 || (XG && CL == 4 && P % 4 == 0), "16-B frame loads: the halo-only form with 16-B frames");
+  static_assert(XL == 0 || (XG && P % 4 == 0), "16-B frame-piece loads: the halo-only form");
   constexpr int QM = G == 4 ? 3 : 7;
   constexpr int NB = 64 / CL;              // CH: frame blocks per wave
   constexpr int WF = NB * P;               // CH: frames per wave
@@ -844,7 +847,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   uint32_t xr[XG ? P : 1];
   auto load_x = [&]() {
     if constexpr (XL == 1) {
-      xl_load<P>(in, t0 + j0, cl, nframes, xr);  // every tile (transposed after the first barrier)
+      xl_load<P, CL>(in, t0 + j0, cl, nframes, xr);  // every tile (transposed after the first barrier)
     } else if (tile_full) {
       const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
 #pragma unroll

@@ -43,7 +43,6 @@ __global__ __launch_bounds__(WG) void pair_ahead_kernel(AheadParams p) {
   constexpr int E = CEl::E;
   constexpr int CL = C / E;  // dword columns per frame (a lane owns one)
   static_assert(C % E == 0 && (CL == 4 || CL == 8), "16- or 32-B frames");
-  static_assert(XL == 0 || CL == 4, "16-B frame loads: 16-B frames");
   constexpr int NB = 64 / CL;   // frame blocks per wave
   constexpr int WF = NB * P;    // frames per wave
   constexpr int TF = NW * WF;   // frames per tile
@@ -103,7 +102,7 @@ __global__ __launch_bounds__(WG) void pair_ahead_kernel(AheadParams p) {
   uint32_t xr0[P], xr1[P];
   auto load_x = [&](long long t0, bool full, uint32_t (&xr)[P]) {
     if constexpr (XL == 1) {
-      xl_load<P>(in, t0 + j0, cl, nframes, xr);
+      xl_load<P, CL>(in, t0 + j0, cl, nframes, xr);
     } else if (full) {
       const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
 #pragma unroll

@@ -106,17 +106,35 @@ template <typename T, typename A, int C>
 void add_xl(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
   if (k <= 4096) {  // the halo-only channel tile's range (fp32 C = 4: k <= 3584, int16 C = 8: k <= 3072)
-    if constexpr (sizeof(T) == 4 && C == 4) {
+    if constexpr (sizeof(T) == 4 && C == 8) {
+      addC<T, A, C, 32, 256, true>(vs, sg, k);
+      addC<T, A, C, 32, 256, true, kNtS, false, 1>(vs, sg, k);
+      addC<T, A, C, 32, 128, true>(vs, sg, k);
+      addC<T, A, C, 32, 128, true, kNtS, false, 1>(vs, sg, k);
+      addC<T, A, C, 16, 256, true, kNtS, false, 1>(vs, sg, k);
+    } else if constexpr (sizeof(T) == 4 && C == 4) {
       addC<T, A, C, 32, 256, true, kNtS, true>(vs, sg, k);
       addC<T, A, C, 32, 256, true, kNtS, true, 1>(vs, sg, k);
+      addC<T, A, C, 16, 256, true, kNtS, true>(vs, sg, k);
       addC<T, A, C, 16, 256, true, kNtS, true, 1>(vs, sg, k);
+      addC<T, A, C, 16, 128, true, kNtS, true, 1>(vs, sg, k);
     } else if constexpr (sizeof(T) == 2 && C == 8) {
       addC<T, A, C, 32, 256, true>(vs, sg, k);
       addC<T, A, C, 32, 256, true, kNtS, false, 1>(vs, sg, k);
+      addC<T, A, C, 16, 256, true>(vs, sg, k);
       addC<T, A, C, 16, 256, true, kNtS, false, 1>(vs, sg, k);
+      addC<T, A, C, 16, 128, true, kNtS, false, 1>(vs, sg, k);
     }
+    if (k < 2048) return;  // (the look-ahead shapes below: 2048-frame tiles)
   }
-  if constexpr (sizeof(T) == 4 && C == 4) {
+  if constexpr (sizeof(T) == 4 && C == 8) {
+    if (k >= 1024) {
+      addAC<T, A, C, 32, 256, 1, 4, true>(vs, sg, k, ws, 384);
+      for (int D : {256, 384, 512}) addAC<T, A, C, 32, 256, 1, 4, true, 0, 1>(vs, sg, k, ws, D);
+      addAC<T, A, C, 16, 256, 1, 2, true, 0, 1>(vs, sg, k, ws, 768);
+      addAC<T, A, C, 64, 256, 1, 8, true, 0, 1>(vs, sg, k, ws, 256);
+    }
+  } else if constexpr (sizeof(T) == 4 && C == 4) {
     addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 768);
     addAC<T, A, C, 16, 256, 1, 4, true, 0, 1>(vs, sg, k, ws, 768);
     for (int D : {256, 320, 384, 448}) addAC<T, A, C, 32, 256, 1, 8, true, 0, 1>(vs, sg, k, ws, D);
@@ -429,8 +447,9 @@ int main(int argc, char** argv) {
   if (xlab) {
     switch (C * (i16 ? -1 : 1)) {
       case 4: add_xl<float, double, 4>(vs, sg, k, w2); break;
+      case 8: add_xl<float, double, 8>(vs, sg, k, w2); break;
       case -8: add_xl<int16_t, int32_t, 8>(vs, sg, k, w2); break;
-      default: fprintf(stderr, "xl: f32 C=4, i16 C=8\n"); return 1;
+      default: fprintf(stderr, "xl: f32 C=4/8, i16 C=8\n"); return 1;
     }
   } else if (pairab) {
     switch (C * (i16 ? -1 : 1)) {
