@@ -32,11 +32,15 @@ def head_frames(grade: int, nframes: int) -> int:
     return min(nframes, (grade - 1 + 63) // 64 * 64)
 
 
-def start_halo_exchange(x_local, grade: int, channels: int = 1, group=None, recv_buf=None):
+def start_halo_exchange(x_local, grade: int, channels: int = 1, group=None, recv_buf=None, peers=None):
     """Post the halo send (this shard's last (grade-1)*channels samples to
     rank+1) and receive (rank-1's tail); returns (requests, history) where
     history is None on rank 0 / grade 1.  Wait on the requests before using
-    history; with NCCL (= RCCL) the wait makes the current stream wait."""
+    history; with NCCL (= RCCL) the wait makes the current stream wait.
+    `peers` = (receive-from, send-to) group ranks (None: no such peer) replaces
+    rank - 1 / rank + 1: a one-rank communicator can then exchange with itself,
+    which is how tests/test_rccl_one_device.py runs this RCCL path on a
+    one-GPU box."""
     import torch
     import torch.distributed as dist
 
@@ -45,25 +49,31 @@ def start_halo_exchange(x_local, grade: int, channels: int = 1, group=None, recv
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     h = (grade - 1) * channels
-    if h == 0 or world == 1:
+    if peers is None:
+        peers = (rank - 1 if rank > 0 else None, rank + 1 if rank + 1 < world else None)
+    src, dst = peers
+    if h == 0 or (src is None and dst is None):
         return [], None
     if x_local.numel() < h:
         raise ValueError(f"shard holds {x_local.numel()} samples < halo {h}: use fewer ranks or a smaller grade")
     # gloo cannot move device tensors: stage the halo through host memory
     # (rehearsal / CPU-only use; the measured multi-GPU path is NCCL = RCCL)
     staged = x_local.is_cuda and dist.get_backend(group) != "nccl"
+    # RCCL's process group takes no int16 ("Short") tensors: the halo moves as its bytes (a uint8
+    # view of the same memory, no copy) -- found by tests/test_rccl_one_device.py on MI355X
+    as_bytes = (lambda t: t.view(torch.uint8)) if not staged and dist.get_backend(group) == "nccl" else (lambda t: t)
     ops = []
-    if rank + 1 < world:
+    if dst is not None:
         tail = x_local[x_local.numel() - h:]
         if staged:
             tail = tail.cpu()
-        ops.append(dist.P2POp(dist.isend, tail, _peer(rank + 1, group), group))
+        ops.append(dist.P2POp(dist.isend, as_bytes(tail), _peer(dst, group), group))
     hist = None
     wire = None
-    if rank > 0:
+    if src is not None:
         hist = recv_buf if recv_buf is not None else torch.empty(h, dtype=x_local.dtype, device=x_local.device)
         wire = torch.empty(h, dtype=x_local.dtype) if staged else hist
-        ops.append(dist.P2POp(dist.irecv, wire, _peer(rank - 1, group), group))
+        ops.append(dist.P2POp(dist.irecv, as_bytes(wire), _peer(src, group), group))
     reqs = dist.batch_isend_irecv(ops) if ops else []
     if staged and wire is not None:
         reqs = [_StagedRecv(reqs, wire, hist)]

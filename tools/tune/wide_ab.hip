@@ -385,10 +385,17 @@ void add_wide_i16(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     add1<T, A, C, 16, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 8, 2, 256, 0>(vs, sg, k);
     add1<T, A, C, 8, 1, 512, 0>(vs, sg, k);  // 4096-frame tiles: a quarter of the tile's halo
+    // round 6: 1024-frame tiles (128 threads; 32-B chunks are not a chunk shape)
+    add1<T, A, C, 8, 1, 128, 0>(vs, sg, k);
+    if (getenv("WIDE_AB_TILES_ONLY")) return;
   } else if constexpr (C == 8) {
     add1<T, A, C, 8, 1, 256, 0>(vs, sg, k);
     add1<T, A, C, 8, 1, 256, 1>(vs, sg, k);  // the magic-multiply division
     add1<T, A, C, 4, 2, 256, 0>(vs, sg, k);
+    // round 6: 1024-frame tiles (half the stage: 5 workgroups per CU by LDS)
+    add1<T, A, C, 4, 1, 256, 0>(vs, sg, k);
+    add1<T, A, C, 8, 1, 128, 0>(vs, sg, k);
+    if (getenv("WIDE_AB_TILES_ONLY")) return;
     // the halo-only channel-per-lane look-ahead (82 VGPRs) at tile-scan windows too
     addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 384);
     addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 512);
