@@ -535,12 +535,14 @@ int dispatch_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws) {
 // wide look-ahead scan (mavg_wide.hpp): the look-ahead record carry in its
 // unit layout (F frames x U units per lane, per-tile records) with the wide
 // in-tile scan (P-frame chunks x UW rows); 16-B-aligned views only.
-// self: aggregate-first (self-published) records, the int16 halo-only CH form only (wide_ahead_kernel)
+// self: aggregate-first (self-published) records, the halo-only CH form only (wide_ahead_kernel: every
+// producer forms a record in one order, so fp32 records keep their bits too)
 template <typename T, typename A, int C, int P, int UW, int WG, int NT, int DV, int F, int U, bool CH = false,
           bool XG = false, int MW = 0, int XL = 0>
 int launch_wide_ahead(const Sig& sg, int k, hipStream_t st, Workspace ws, int ahead, bool self = false) {
   // (self + XL: the self-published record would be summed before the quad transposes)
-  if (self && !(CH && XG && std::is_integral<T>::value && XL == 0)) return MAVG_ERR_UNSUPPORTED;
+  if (self && !(CH && XG && XL != 1)) return MAVG_ERR_UNSUPPORTED;
+  if (XL == 2 && !self) return MAVG_ERR_UNSUPPORTED;  // XL = 2: the columns formed before the self-published record
   constexpr int NW = WG / 64;
   constexpr int EPG = 16 / (int)sizeof(T);
   constexpr int CL = C * (int)sizeof(T) / 4 > 0 ? C * (int)sizeof(T) / 4 : 1;  // CH: dword columns per frame
@@ -774,6 +776,17 @@ int dispatch_scan_f(const Sig& sg, int k, int block, hipStream_t st, Workspace w
 //   Kept on the unit kernels: fp32 mono and int16 mono/stereo (a tie or a
 //   loss: int16 stereo k=1024 0.786 vs 0.788, k=44100 0.631 vs 0.587; fp32
 //   mono k=44100 0.677 vs 0.663).
+// The 2048-frame halo-only channel-per-lane look-ahead with 16-B frames (fp32 4 channels, int16 8
+// channels): self-published records, except fp32 at windows of whole tiles (k mod 2048 = 0), where
+// in bench.py's environment phase A measured ahead (k = 8192 0.666-0.670 vs 0.656-0.657, 16384
+// 0.670 vs 0.647, 32768 0.666 vs 0.637, 4096 a tie; elsewhere self-published wins by 4-6 %).  int16
+// 8 channels: self-published at every window (k = 4096 0.660 vs 0.631, 8192 0.651 vs 0.632,
+// 16384 / 32768 ties).  profiles/r06_tuning/xl/ab_f32c4_*, ab_i16c8_*, ab_selfall_*.
+template <typename T>
+inline bool self_pays(int k) {
+  return sizeof(T) == 2 || k % 2048 != 0;  // (int16 8 channels: always)
+}
+
 template <typename T, typename A, int C>
 int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
   constexpr int kNtS = kNtSplit | kNtHalo | kNtStore;
@@ -807,6 +820,7 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     // past the chan tile: the halo-only channel-per-lane look-ahead (round 5, in-process,
     // profiles/r05_tuning/wide/pa0_c4_k44100.log: k=44100 0.540 -> 0.593 against the chunk
     // look-ahead), with XL in 2048-frame tiles (above)
+    if (self_pays<T>(k)) return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 8, true, true, 0, 2>(sg, k, st, ws, 384, true);
     return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 8, true, true, 0, 1>(sg, k, st, ws, 384);
   } else if constexpr (sizeof(T) == 4 && C == 8) {
     // one channel per lane (chan_tile_kernel, 32 frames each): one scan per
@@ -851,13 +865,16 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
       // a window of at least the tile: the halo-only channel-per-lane tile, a dword column (two
       // channels) per lane (round 5, in-process, profiles/r05_tuning/wide/i16_c8_k2048.log: k=2048
       // 0.589 -> 0.652 against the wide tile)
-      if (halo_bytes <= 49152) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
+      if (halo_bytes <= 32768) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
     }
-    // past it the halo-only channel-per-lane look-ahead (int32 sums: k <= 65535), with x as 16-B
-    // frame loads (XL, round 6; in-process, profiles/r06_tuning/xl/: k = 44100 0.592-0.600 ->
-    // 0.609, 20000 0.600-0.612 -> 0.624, 3072 0.611 -> 0.625)
+    // past it (k > 2048) the halo-only channel-per-lane look-ahead (int32 sums: k <= 65535), x as
+    // 16-B frame pieces (XL) and self-published records (aggregate-first).  In bench.py's
+    // environment against the round-5 shapes (the chan tile to k = 3072, then phase A with XL;
+    // tools/tune/ab_libs.py, profiles/r06_tuning/xl/ab_i16c8_*, outputs bitwise equal): k = 44100
+    // 0.594 -> 0.625, 20000 0.611 -> 0.644, 10000 0.614 -> 0.656, 3072 0.598 -> 0.652, 2560
+    // 0.617 -> 0.657.  (In-process: self-published without XL lost, 0.574 vs 0.596 at k = 44100.)
     if constexpr (sizeof(A) == 4)
-      return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 8, true, true, 0, 1>(sg, k, st, ws, 384);
+      return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 8, true, true, 0, 2>(sg, k, st, ws, 384, true);
     return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);
   }
   (void)halo_bytes;

@@ -833,12 +833,15 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   const unsigned nb = gridDim.x;
   const unsigned bd = blockIdx.x + (unsigned)p.ahead;
   const long long ja = bd < nb ? map_tile(bd) : -1;
-  // SELF (round 6, int16 halo-only CH form only; AheadParams::self): aggregate-first records --
-  // no phase A; every tile publishes its own record from the x it holds in registers as soon as
-  // its loads land, and the carry reads the records after the in-tile scan.  Integer sums are
-  // exact, so a record summed in the lane / butterfly order here has the bits of the producer's
-  // and the recompute path's sequences: the output is the same under every schedule.
-  constexpr bool kSelfOk = CH && XG && std::is_integral<T>::value;
+  // SELF (round 6, the halo-only CH form; AheadParams::self): aggregate-first records -- no phase
+  // A; every tile publishes its own record from the x it holds in registers as soon as its loads
+  // land, and the carry reads the records after the in-tile scan.  Every producer of a record in
+  // this mode -- the tile itself, head duty, a consumer's recompute -- forms it in one order: per
+  // wave, each lane's column summed over its P frames in frame order, then butterflies over the
+  // lanes of the column (strides CL .. 32), then the NW waves' shares added in wave order
+  // (publish_record_lds).  So the record has the same bits whoever computes it, for fp64 sums of
+  // fp32 as for integer sums, and the output is the same under every schedule.
+  constexpr bool kSelfOk = CH && XG;
   const bool self = kSelfOk && p.self != 0;
   const bool produce = !self && ja >= 0 && ja < p.nfull;
   // XG: the lane's x (dword column cl -- channels cl*E .. cl*E + E - 1 -- of frames j0 .. j0 + P - 1)
@@ -846,7 +849,7 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
   const int j0 = w * WF + (lane / CL) * P;
   uint32_t xr[XG ? P : 1];
   auto load_x = [&]() {
-    if constexpr (XL == 1) {
+    if constexpr (XL >= 1) {
       xl_load<P, CL>(in, t0 + j0, cl, nframes, xr);  // every tile (transposed after the first barrier)
     } else if (tile_full) {
       const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
@@ -924,23 +927,35 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
     share(0, r);
   }
   if (tid == 0) MAVG_ATRACE(1, MAVG_ANOW());
+  // XL = 2 (with self-published records only): the columns are formed right away, since the record
+  // below sums them as soon as the loads land anyway
+  if constexpr (XL == 2) xl_transpose<P>(xr, cl);
   const bool own = (self || blockIdx.x < (unsigned)p.ahead) && tile < p.nfull;  // no block D slots earlier
+  // SELF: the wave's share of a record in the self order, from the column values x(i) of the
+  // frames of this wave's part of the tile: the lane's column sums over i in frame order, then
+  // butterflies over the lanes of one column; lanes < CL hold the column totals
+  auto self_share = [&](int src, auto xcol) {
+    SA sc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) sc[e] = (SA)0;
+    xcol(sc);
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int sh = CL; sh < 64; sh <<= 1) sc[e] += __shfl_xor(sc[e], sh, 64);
+    if (lane < CL)
+#pragma unroll
+      for (int e = 0; e < E; ++e) shares[(src * NW + w) * C + lane * E + e] = sc[e];
+  };
   if (own) {
     if constexpr (kSelfOk) {
-      if (self) {  // the lane's column sums, then butterflies over the lanes of one column
-        SA sc[E];
+      if (self)
+        self_share(1, [&](SA (&sc)[E]) {
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-          sc[e] = (SA)0;
+          for (int e = 0; e < E; ++e)
 #pragma unroll
-          for (int i = 0; i < P; ++i) sc[e] += to_acc<SA>(CEl::get(xr[i], e));
-#pragma unroll
-          for (int sh = CL; sh < 64; sh <<= 1) sc[e] += __shfl_xor(sc[e], sh, 64);
-        }
-        if (lane < CL)
-#pragma unroll
-          for (int e = 0; e < E; ++e) shares[(1 * NW + w) * C + lane * E + e] = sc[e];
-      }
+            for (int i = 0; i < P; ++i) sc[e] += to_acc<SA>(CEl::get(xr[i], e));
+        });
     }
     if (!self) {
       SA r[C];
@@ -956,10 +971,25 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
       if (j >= 0 && j < p.nfull) jh = j;
     }
   }
+  // the column loads of the rare paths (head duty, recompute): frame j*TF + wave*WF + block*P + i
+  const uint32_t* in32c = reinterpret_cast<const uint32_t*>(in);
   if (jh >= 0) {
-    SA r[C];
-    wave_record_lean<T, SA, C, F, U, WG>(in, jh, w, lane, false, r);
-    share(2, r);
+    if constexpr (kSelfOk) {
+      if (self)
+        self_share(2, [&](SA (&sc)[E]) {
+#pragma unroll 1
+          for (int i = 0; i < P; ++i) {
+            const uint32_t x = in32c[(jh * TF + j0 + i) * CL + cl];
+#pragma unroll
+            for (int e = 0; e < E; ++e) sc[e] += to_acc<SA>(CEl::get(x, e));
+          }
+        });
+    }
+    if (!self) {
+      SA r[C];
+      wave_record_lean<T, SA, C, F, U, WG>(in, jh, w, lane, false, r);
+      share(2, r);
+    }
   }
   // the carry reads one (record, channel) pair per thread: slot s = q*C + c
   // (C x fewer registers held across the scan than whole records per thread;
@@ -1190,10 +1220,34 @@ __global__ __launch_bounds__(WG, MW > 0 ? MW : 1) void wide_ahead_kernel(AheadPa
       // one channel at a time (the producer's additions for that channel, the
       // same bits): one accumulator live instead of a whole record's C
       SA v = (SA)0;
+      if (self) {
+        // the self order (SELF above): this wave plays each producer wave in turn, every lane its
+        // own column's element e; lane ch / E then holds channel ch's share of that wave
+        if constexpr (kSelfOk) {
 #pragma unroll 1
-      for (int c = 0; c < C; ++c) {
-        const SA rc = tile_record_chan_lean<T, SA, C, F, U, WG>(in, qlo + ql, c, lane);
-        if (cc == c) v = rc;
+          for (int e = 0; e < E; ++e) {
+            SA r = (SA)0;
+#pragma unroll 1
+            for (int wv = 0; wv < NW; ++wv) {
+              SA sw = (SA)0;
+              const long long fb = (qlo + ql) * TF + wv * WF + (lane / CL) * P;
+#pragma unroll 1
+              for (int i = 0; i < P; ++i) sw += to_acc<SA>(CEl::get(in32c[(fb + i) * CL + cl], e));
+#pragma unroll
+              for (int sh = CL; sh < 64; sh <<= 1) sw += __shfl_xor(sw, sh, 64);
+              r = wv == 0 ? sw : r + sw;  // publish_record_lds: the shares in wave order
+            }
+            // channel cc = column cc / E, element cc mod E: lane cc / E holds that column's total
+            const SA t = __shfl(r, cc / E, 64);
+            if (cc % E == e) v = t;
+          }
+        }
+      } else {
+#pragma unroll 1
+        for (int c = 0; c < C; ++c) {
+          const SA rc = tile_record_chan_lean<T, SA, C, F, U, WG>(in, qlo + ql, c, lane);
+          if (cc == c) v = rc;
+        }
       }
       const bool mine = miss && sl / C == ql;
       if (mine) {

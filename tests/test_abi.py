@@ -188,10 +188,13 @@ def test_plan_describes_launch_without_gpu():
     # past the halo-only tile (8 channels k > 1536, 4 channels k > 3584): the halo-only channel-per-lane
     # look-ahead (x from global memory, only the shifted tile in LDS)
     # (round 6: with 16-B frames x comes as whole-frame loads turned into columns, xl=1)
-    for C, k in ((8, 1537), (8, 44100), (4, 2561), (4, 3000), (4, 3088), (4, 44100)):
+    for C, k in ((8, 1537), (8, 44100), (4, 2561), (4, 3000), (4, 3088), (4, 8192), (4, 44100)):
         p = dsp.plan(1 << 30, k, channels=C)
         assert p.startswith(f"wide_ahead<f32,acc=f64,C={C},P=32") and ",ch=1,xg=1," in p, p
-        assert (",xl=1>" in p) == (C == 4), p
+        # 4 channels: self-published records with the columns formed at once (xl=2), phase A with
+        # XL at windows of whole 2048-frame tiles (xl=1); 8 channels: phase A, column loads
+        want = ",xl=0>" if C == 8 else (",xl=1>" if k % 2048 == 0 else ",xl=2>")
+        assert want in p and ((" self=1 " in p) == (want == ",xl=2>")), p
     assert ",xg=1>" in dsp.plan(1 << 30, 1536, channels=8)
     for k in (2048, 2544, 2560, 3072):  # the in-place chan tile (staged halo of exactly k frames),
         p = dsp.plan(1 << 30, k, channels=4)  # with XL while 4 workgroups per CU fit its LDS (160 KiB)
@@ -201,7 +204,9 @@ def test_plan_describes_launch_without_gpu():
     i16c8 = lambda k: dsp.plan(1 << 30, k, channels=8, dtype=dsp.I16)
     assert i16c8(1024).startswith("wide_tile<i16") and i16c8(2048).startswith("chan_tile<i16,acc=i32,C=8,Q=32")
     assert i16c8(44100).startswith("wide_ahead<i16,acc=i32,C=8,P=32") and ",ch=1,xg=1," in i16c8(44100)
-    assert ",xl=1>" in i16c8(44100) and ",xl=1>" in i16c8(3073)
+    for k in (2049, 3073, 8192, 44100):  # past the chan tile: self-published, columns formed at once
+        assert ",xl=2>" in i16c8(k) and " self=1 " in i16c8(k), i16c8(k)
+    assert i16c8(2048).startswith("chan_tile<i16")
     # aggregate-first look-ahead records in 32-KiB tiles (round 6): int16 mono / stereo past a
     # 16-KiB halo, int16 4 channels past 64 KiB, fp32 stereo past the wide tile's 32 KiB, short of
     # the L2 reach (int16 mono: k <= 131072); fp32 mono and 8 channels keep their kernels

@@ -796,7 +796,8 @@ def test_f32_multichannel_long_windows_every_form(oracle_mod, gpu, C, k):
     assert_f32_close(_run(x, k, C, "blelloch_scalar", gpu), ref, f"k={k} scalar")
 
 
-@pytest.mark.parametrize("C,k", [(2, 300_000), (4, 3585), (4, 20_000), (8, 2049), (8, 44_100), (8, 700_000)])
+@pytest.mark.parametrize("C,k", [(2, 300_000), (4, 3585), (4, 20_000), (4, 8192), (8, 2049), (8, 44_100),
+                                 (8, 700_000)])
 def test_wide_ahead_bitwise_whatever_the_schedule(oracle_mod, gpu, C, k):
     """Multi-channel fp32 windows past the wide tile run the wide look-ahead
     scan (stereo: past the L2 reach; shorter stereo windows take the
@@ -804,7 +805,10 @@ def test_wide_ahead_bitwise_whatever_the_schedule(oracle_mod, gpu, C, k):
     and bitwise the same output when every record is recomputed by its
     consumer (spin 0), under the one-pass (slots 0) and minimal look-ahead
     schedules (the debug build's schedule hook) as under the release build's
-    default schedule; ragged XCD runs and a ragged tail tile."""
+    default schedule; ragged XCD runs and a ragged tail tile.  fp32 4 channels
+    (round 6) publish every record in one order from every producer -- the tile
+    itself, head duty, a consumer's recompute -- so self-published fp64 records
+    keep their bits too (k = 3585, 20000; k = 8192: phase A)."""
     import digital_signal_processsing_amd as dsp
     frames = max(2_600_000 // C, 3 * k) + 12_345
     plan = dsp.plan(frames * C, k, C, dsp.F32)

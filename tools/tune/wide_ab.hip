@@ -95,7 +95,7 @@ void addAC(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws, int D, bool
   constexpr int kNtA = kNtStore | kNtHalo;
   char name[80];
   snprintf(name, sizeof name, "wahead chan Q%d %d F%d U%d D%d xg%d mw%d%s%s", Q, WG, F, U, D, (int)XG, MW,
-           self ? " self" : "", XL ? " xl1" : "");
+           self ? " self" : "", XL == 2 ? " xl2" : (XL ? " xl1" : ""));
   vs.push_back({name, [=](hipStream_t s) {
                   return launch_wide_ahead<T, A, C, Q, 1, WG, kNtA, 0, F, U, true, XG, MW, XL>(sg, k, s, ws, D, self);
                 }, {}});
@@ -130,11 +130,21 @@ void add_xl(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
   if constexpr (sizeof(T) == 4 && C == 8) {
     if (k >= 1024) {
       addAC<T, A, C, 32, 256, 1, 4, true>(vs, sg, k, ws, 384);
+      // round 6: self-published records in the one order every producer uses (fp32 too)
+      addAC<T, A, C, 32, 256, 1, 4, true>(vs, sg, k, ws, 384, true);
+      addAC<T, A, C, 32, 256, 1, 4, true, 0, 2>(vs, sg, k, ws, 384, true);
+      if (getenv("WIDE_AB_SELF_ONLY")) return;
       for (int D : {256, 384, 512}) addAC<T, A, C, 32, 256, 1, 4, true, 0, 1>(vs, sg, k, ws, D);
       addAC<T, A, C, 16, 256, 1, 2, true, 0, 1>(vs, sg, k, ws, 768);
       addAC<T, A, C, 64, 256, 1, 8, true, 0, 1>(vs, sg, k, ws, 256);
     }
   } else if constexpr (sizeof(T) == 4 && C == 4) {
+    // round 6: self-published records in the one order every producer uses (fp32 too)
+    addAC<T, A, C, 32, 256, 1, 8, true, 0, 1>(vs, sg, k, ws, 384);
+    addAC<T, A, C, 32, 256, 1, 8, true, 0, 2>(vs, sg, k, ws, 384, true);
+    addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 384, true);
+    addAC<T, A, C, 16, 256, 1, 4, true, 0, 2>(vs, sg, k, ws, 768, true);
+    if (getenv("WIDE_AB_SELF_ONLY")) return;
     addAC<T, A, C, 16, 256, 1, 4, true>(vs, sg, k, ws, 768);
     addAC<T, A, C, 16, 256, 1, 4, true, 0, 1>(vs, sg, k, ws, 768);
     for (int D : {256, 320, 384, 448}) addAC<T, A, C, 32, 256, 1, 8, true, 0, 1>(vs, sg, k, ws, D);
@@ -143,9 +153,14 @@ void add_xl(std::vector<Var>& vs, const Sig& sg, int k, Workspace ws) {
     addP<T, A, C, 16, 256, 4, 1>(vs, sg, k, ws, 768);
     addP<T, A, C, 16, 256, 4, 1>(vs, sg, k, ws, 1024);
   } else if constexpr (sizeof(T) == 2 && C == 8) {
+    addAC<T, A, C, 32, 256, 1, 8, true, 0, 1>(vs, sg, k, ws, 384);
+    addAC<T, A, C, 32, 256, 1, 8, true, 0, 2>(vs, sg, k, ws, 384, true);
+    if (getenv("WIDE_AB_SELF_ONLY")) return;
     addAC<T, A, C, 32, 256, 1, 8, true>(vs, sg, k, ws, 384);
     for (int D : {384, 512, 640}) addAC<T, A, C, 32, 256, 1, 8, true, 0, 1>(vs, sg, k, ws, D);
-    addAC<T, A, C, 32, 512, 1, 8, true, 0, 1>(vs, sg, k, ws, 384, true);
+    addAC<T, A, C, 32, 512, 1, 8, true, 0, 2>(vs, sg, k, ws, 384, true);  // XL = 2: self-published
+    addAC<T, A, C, 32, 256, 1, 8, true, 0, 2>(vs, sg, k, ws, 384, true);
+    addAC<T, A, C, 32, 512, 1, 8, true>(vs, sg, k, ws, 384, true);
     addAC<T, A, C, 32, 512, 1, 8, true, 0, 1>(vs, sg, k, ws, 384);
     addP<T, A, C, 16, 256, 4, 1>(vs, sg, k, ws, 768);
   }
