@@ -28,7 +28,7 @@ def main(path, traffic_path=None):
         r = d["roofline"]
         kern = r["kernel"].split(" grid")[0]
         fam = kern.split("<")[0]
-        tags = [t for t in ("ch=1", "xg=1", "ip=1", "xl=1", "hillis", "self=1", "runs=1") if t in r["kernel"]]
+        tags = [t for t in ("ch=1", "xg=1", "ip=1", "xl=1", "xl=2", "hillis", "self=1", "runs=1") if t in r["kernel"]]
         t = traffic.get(f"{name}:{d['config']['algo']}", {}).get("traffic_over_algorithmic")
         print(f"| {name} | {fam}{' ' + ','.join(tags) if tags else ''} | {d['value']:.0f} | {r['frac']:.3f} | "
               f"{r.get('frac_of_copy', float('nan')):.3f} | {t if t is not None else '—'} |")
