@@ -77,8 +77,8 @@ WORKLOADS = {
     "f32_c4_long": (1 << 30, 44100, 4, "f32", "blelloch"),
     "f32_c8_long": (1 << 30, 44100, 8, "f32", "blelloch"),
     "f32_c8_k2048": (1 << 30, 2048, 8, "f32", "blelloch"),
-    # the in-place halo-only channel tile (fp32 C = 4) and the int16 dword-column channel tile
-    # (C = 8) at the window where each is dispatched
+    # the in-place halo-only channel tile (fp32 C = 4) and the int16 dword-column look-ahead (C = 8,
+    # self-published records) at a window of one tile
     "f32_c4_k2048": (1 << 30, 2048, 4, "f32", "blelloch"),
     "i16_c8_k2048": (1 << 30, 2048, 8, "i16", "blelloch"),
     "i16_c4_2p30": (1 << 30, 1024, 4, "i16", "blelloch"),

@@ -862,17 +862,15 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     if constexpr (sizeof(A) == 4) {
       if (halo_bytes <= 256) return launch_wide_tile<T, A, C, 8, 1, 128, kNtS>(sg, k, st);
       if (halo_bytes < 32768) return launch_wide_tile<T, A, C, 8, 1, kWG, kNtS>(sg, k, st);
-      // a window of at least the tile: the halo-only channel-per-lane tile, a dword column (two
-      // channels) per lane (round 5, in-process, profiles/r05_tuning/wide/i16_c8_k2048.log: k=2048
-      // 0.589 -> 0.652 against the wide tile)
-      if (halo_bytes <= 32768) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true>(sg, k, st);
     }
-    // past it (k > 2048) the halo-only channel-per-lane look-ahead (int32 sums: k <= 65535), x as
-    // 16-B frame pieces (XL) and self-published records (aggregate-first).  In bench.py's
-    // environment against the round-5 shapes (the chan tile to k = 3072, then phase A with XL;
-    // tools/tune/ab_libs.py, profiles/r06_tuning/xl/ab_i16c8_*, outputs bitwise equal): k = 44100
-    // 0.594 -> 0.625, 20000 0.611 -> 0.644, 10000 0.614 -> 0.656, 3072 0.598 -> 0.652, 2560
-    // 0.617 -> 0.657.  (In-process: self-published without XL lost, 0.574 vs 0.596 at k = 44100.)
+    // a window of at least the tile (k >= 2048): the halo-only channel-per-lane look-ahead, a dword
+    // column (two channels) per lane (int32 sums: k <= 65535), x as 16-B frame pieces (XL) and
+    // self-published records (aggregate-first).  In bench.py's environment against the round-5
+    // shapes (the halo-only chan tile to k = 3072, then phase A with XL; tools/tune/ab_libs.py,
+    // profiles/r06_tuning/xl/ab_i16c8_*, ab_nochan_*, outputs bitwise equal): k = 44100 0.594 ->
+    // 0.625, 20000 0.611 -> 0.644, 10000 0.614 -> 0.656, 3072 0.598 -> 0.652, 2560 0.617 -> 0.657,
+    // 2048 0.652 -> 0.672 (so int16 no longer takes the chan tile).  (In-process: self-published
+    // without XL lost, 0.574 vs 0.596 at k = 44100.)
     if constexpr (sizeof(A) == 4)
       return launch_wide_ahead<T, A, C, 32, 1, kWG, kNtA, 0, 1, 8, true, true, 0, 2>(sg, k, st, ws, 384, true);
     return launch_wide_ahead<T, A, C, 4, 1, kWG, kNtA, 0, 1, 4>(sg, k, st, ws, 1024);

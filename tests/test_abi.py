@@ -202,11 +202,11 @@ def test_plan_describes_launch_without_gpu():
         assert p.startswith("chan_tile<f32,acc=f64,C=4,Q=32") and want in p, p
     # int16 8 channels: a dword column (two channels) per lane from a window of one tile on
     i16c8 = lambda k: dsp.plan(1 << 30, k, channels=8, dtype=dsp.I16)
-    assert i16c8(1024).startswith("wide_tile<i16") and i16c8(2048).startswith("chan_tile<i16,acc=i32,C=8,Q=32")
+    assert i16c8(1024).startswith("wide_tile<i16") and i16c8(2047).startswith("wide_tile<i16")
     assert i16c8(44100).startswith("wide_ahead<i16,acc=i32,C=8,P=32") and ",ch=1,xg=1," in i16c8(44100)
-    for k in (2049, 3073, 8192, 44100):  # past the chan tile: self-published, columns formed at once
-        assert ",xl=2>" in i16c8(k) and " self=1 " in i16c8(k), i16c8(k)
-    assert i16c8(2048).startswith("chan_tile<i16")
+    for k in (2048, 2049, 3073, 8192, 44100):  # past the wide tile: self-published, columns formed at once
+        assert i16c8(k).startswith("wide_ahead<i16,acc=i32,C=8,P=32") and ",xl=2>" in i16c8(k), i16c8(k)
+        assert " self=1 " in i16c8(k), i16c8(k)
     # aggregate-first look-ahead records in 32-KiB tiles (round 6): int16 mono / stereo past a
     # 16-KiB halo, int16 4 channels past 64 KiB, fp32 stereo past the wide tile's 32 KiB, short of
     # the L2 reach (int16 mono: k <= 131072); fp32 mono and 8 channels keep their kernels

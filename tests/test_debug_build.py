@@ -121,9 +121,9 @@ for C, k in ((1, 20_000), (2, 44_100), (4, 9_000)):
     assert p.startswith("ahead_scan<i16") and "self=1" in p and "U=8" in p, p
     xs = oracle.synth_i16(100_003 * C, seed=k)
     assert np.array_equal(run(xs, k, C, "auto"), oracle.mavg_i16(xs, k, C)), (C, k)
-# int16 with 8 channels: the dword-column (two channels per lane) chan tile and, past k = 2048, the
-# look-ahead with self-published records (round 6)
-for k, kern in ((2048, "chan_tile<i16"), (3000, "wide_ahead<i16"), (20_000, "wide_ahead<i16")):
+# int16 with 8 channels: from k = 2048 the dword-column (two channels per lane) look-ahead with
+# self-published records (round 6)
+for k, kern in ((2048, "wide_ahead<i16"), (3000, "wide_ahead<i16"), (20_000, "wide_ahead<i16")):
     assert dsp.plan(100_003 * 8, k, 8, dsp.I16).startswith(kern), k
     xs = oracle.synth_i16(100_003 * 8, seed=k)
     assert np.array_equal(run(xs, k, 8, "auto"), oracle.mavg_i16(xs, k, 8)), k

@@ -49,7 +49,7 @@ CONFIGS = [
     ("i16_c8_2p30_k1024", 1 << 30, 1024, 8, "i16", "blelloch"),
     ("i16_c4_2p30_k44100", 1 << 30, 44100, 4, "i16", "blelloch"),
     ("i16_c8_2p30_k44100", 1 << 30, 44100, 8, "i16", "blelloch"),
-    # the int16 dword-column chan tile (C = 8, k = 2048; past it the self-published look-ahead) at full size
+    # int16 8 channels at a window of one tile: the dword-column look-ahead, self-published (round 6)
     ("i16_c8_2p30_k2048", 1 << 30, 2048, 8, "i16", "blelloch"),
     # the chunk-form wide look-ahead (fp32 stereo past the L2 reach, int16 8 channels past int32
     # sums) with a partial window (k mod tile != 0): the r05ad development build zeroed that part
