@@ -813,6 +813,8 @@ int dispatch_wide(const Sig& sg, int k, hipStream_t st, Workspace ws) {
     const bool ip = k % 16 == 0;  // the staged halo is exactly k frames (chan tile IP)
     if (k >= 2048 && k <= 3072 && ip) {
       if (halo_bytes <= 40704) return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true, true, 1>(sg, k, st);
+      // (three workgroups per CU: still ahead of the self-published look-ahead in bench.py's
+      // environment, k = 2560 0.718 vs 0.705, 2816 0.709 vs 0.700, 3072 a tie; ab_chan3_*)
       return launch_chan_tile<T, A, C, 32, kWG, kNtS, 0, true, true>(sg, k, st);
     }
     if (halo_bytes <= 4096) return launch_wide_tile<T, A, C, 8, 2, kWG, kNtS>(sg, k, st);
