@@ -820,6 +820,10 @@ def test_wide_ahead_bitwise_whatever_the_schedule(oracle_mod, gpu, C, k):
     for sched in ({}, {"spin": 0}, {"slots": 0}, {"slots": 8, "spin": 0}):
         y = _with_schedule(sched, lambda lib: _run(x, k, C, "auto", gpu, library=lib))
         assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), sched
+    if " self=1 " in plan:
+        # the self-order recompute of every record under the debug build's device checks
+        y = _with_schedule({"spin": 0}, lambda lib: _run(x, k, C, "auto", gpu, library=lib), debug=True)
+        assert np.array_equal(y.view(np.uint8), base.view(np.uint8)), "debug build"
 
 
 @pytest.mark.parametrize("C", [2, 4, 8])
