@@ -36,23 +36,25 @@ constexpr int kNW = kWG / 64;     // waves per workgroup
 template <typename A> __device__ __forceinline__ A to_acc(float x) { return (A)x; }
 template <typename A> __device__ __forceinline__ A to_acc(int16_t x) { return (A)x; }
 
-// 64-lane DPP move with zero fill for invalid / masked lanes.
+// 64-lane DPP move with zero fill for invalid / masked lanes: old = 0 for the rows row_mask
+// leaves unwritten, bound_ctrl for source lanes outside the row (with full masks every lane is
+// then written, so the compiler drops the zero init of the destination)
 template <int CTRL, int RM, int BM>
 __device__ __forceinline__ int32_t dpp(int32_t v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, BM, false);
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, BM, true);
 }
 template <int CTRL, int RM, int BM>
 __device__ __forceinline__ double dpp(double v) {
   int lo = __double2loint(v), hi = __double2hiint(v);
-  lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, BM, false);
-  hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, BM, false);
+  lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, BM, true);
+  hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, BM, true);
   return __hiloint2double(hi, lo);
 }
 template <int CTRL, int RM, int BM>
 __device__ __forceinline__ int64_t dpp(int64_t v) {
   int lo = (int)(uint32_t)v, hi = (int)(uint32_t)((uint64_t)v >> 32);
-  lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, BM, false);
-  hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, BM, false);
+  lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, BM, true);
+  hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, BM, true);
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
@@ -92,6 +94,30 @@ __device__ __forceinline__ A wave_incl_scan(A v) {
   v += dpp<0x142, 0xa, 0xf>(v);
   v += dpp<0x143, 0xc, 0xf>(v);
   return v;
+}
+
+// N independent inclusive scans, step by step across the N values (each value sees the same
+// six additions in the same order as wave_incl_scan): the DPP moves of one value fill the wait
+// states after the previous value's add instead of s_nops on one dependent chain
+template <typename A, int N>
+__device__ __forceinline__ void wave_incl_scan_n(A (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x111, 0xf, 0xf>(v[i]);
+  __builtin_amdgcn_sched_barrier(0);  // keep the steps apart: the scheduler would chain them
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x112, 0xf, 0xf>(v[i]);
+  __builtin_amdgcn_sched_barrier(0);  // keep the steps apart: the scheduler would chain them
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x114, 0xf, 0xf>(v[i]);
+  __builtin_amdgcn_sched_barrier(0);  // keep the steps apart: the scheduler would chain them
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x118, 0xf, 0xf>(v[i]);
+  __builtin_amdgcn_sched_barrier(0);  // keep the steps apart: the scheduler would chain them
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x142, 0xa, 0xf>(v[i]);
+  __builtin_amdgcn_sched_barrier(0);  // keep the steps apart: the scheduler would chain them
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x143, 0xc, 0xf>(v[i]);
 }
 
 __device__ __forceinline__ int32_t readlane(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }

@@ -693,6 +693,8 @@ __global__ __launch_bounds__(WG_) void ahead_scan_kernel(AheadParams p) {
       SA run[C];
 #pragma unroll
       for (int c = 0; c < C; ++c) run[c] = (SA)0;
+      // (one scan at a time: the side-by-side scans of the tile kernel's HS form,
+      // wave_incl_scan_n, measured 1 % slower here, tools/gpu/r06_dpp_ab.sh)
 #pragma unroll
       for (int r = 0; r < F; ++r) {
         const int fl = sb + r * 64 + lane;

@@ -218,17 +218,24 @@ __global__ __launch_bounds__(WG) void tile_scan_kernel(TileParams p) {
       A run[C];
 #pragma unroll
       for (int c = 0; c < C; ++c) run[c] = (A)0;
+      // the F*C log-step scans of the segment side by side (wave_incl_scan_n), then the
+      // carries across the F registers in register order
+      A incl[F * C];
 #pragma unroll
       for (int r = 0; r < F; ++r) {
         const int fl = sb + r * 64 + lane;
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-          const A d = to_acc<A>(stage[(Ha + fl) * C + c]) - to_acc<A>(stage[(Ha + fl - k) * C + c]);
-          const A incl = wave_incl_scan(d);
-          v[u][r][c] = incl + run[c];
-          run[c] += readlane(incl, 63);
-        }
+        for (int c = 0; c < C; ++c)
+          incl[r * C + c] = to_acc<A>(stage[(Ha + fl) * C + c]) - to_acc<A>(stage[(Ha + fl - k) * C + c]);
       }
+      wave_incl_scan_n(incl);
+#pragma unroll
+      for (int r = 0; r < F; ++r)
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          v[u][r][c] = incl[r * C + c] + run[c];
+          run[c] += readlane(incl[r * C + c], 63);
+        }
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         lx[u][c] = (A)0;
